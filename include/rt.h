@@ -1,0 +1,169 @@
+/*
+ * rt.h — C ABI of the MI355X path tracer (drop-in for the reference's Camera.render()).
+ *
+ * The reference (AndrewJarrett/raytracing-with-zig, Zig 0.14) has no FFI of its own.  The cut is
+ * `Camera.render(self: Camera) !void` (src/camera.zig:123-145), called from src/main.zig:35.  A Zig
+ * shim marshals the Camera fields (camera.zig:82-103), the Hittable list
+ * (hittable.zig:43-44, Sphere sphere.zig:13-16, Material material.zig:126-143) and the scene
+ * interval/seed (Scene.zig:19-21) into the plain structs below and calls rt_render(), then keeps
+ * its own PPM.saveBinary (ppm.zig:42-60, camera.zig:144).
+ *
+ * Everything is plain C: pointers + sizes, no torch / HIP types in the signatures (device pointers
+ * and streams are passed as void*).  All functions return 0 on success and a negative rt_status on
+ * failure; rt_last_error() returns a thread-local message for the last failure.
+ *
+ * Arithmetic contract: IEEE f64, no FMA contraction, correctly-rounded sqrt/div, in the exact
+ * operation order of the reference.  The only deviation from the reference is the
+ * RNG stream layout: the reference draws every random number from ONE sequential Xoshiro256++
+ * stream (Scene.zig:29-38), which cannot be parallelised; here every (pixel, sample) owns its own
+ * Xoshiro256++ stream (same generator, same Random.float(f64) conversion) keyed by
+ * rt_sample_key(seed, pixel, sample).  See DESIGN.md "RNG".
+ */
+#ifndef RT_MI355X_H
+#define RT_MI355X_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RT_ABI_VERSION 1
+
+/* ---- status codes ---------------------------------------------------------------------------- */
+typedef enum rt_status {
+    RT_OK = 0,
+    RT_ERR_INVALID = -1,   /* bad argument (n==0, W/H/spp==0, negative radius, bad material...) */
+    RT_ERR_HIP = -2,       /* HIP runtime error (message in rt_last_error) */
+    RT_ERR_NO_DEVICE = -3, /* no gfx950 device visible / extension not built for it */
+    RT_ERR_CAPACITY = -4,  /* scene larger than the kernel's sphere capacity */
+    RT_ERR_IO = -5         /* file I/O (PPM writer) */
+} rt_status;
+
+/* ---- materials: tag of the reference's `Material` union (material.zig:113-117) ---------------- */
+typedef enum rt_material_kind {
+    RT_LAMBERTIAN = 0, /* Lambertian.scatter  material.zig:27-39 */
+    RT_METAL = 1,      /* Metal.scatter       material.zig:55-68 */
+    RT_DIELECTRIC = 2  /* Dielectric.scatter  material.zig:82-103 */
+} rt_material_kind;
+
+/* One Hittable (only `.sphere` exists, hittable.zig:22-27).  Replaces Sphere{center, radius, mat}
+ * (sphere.zig:13-16).  The Material's `*DefaultPrng` pointer does not cross the boundary.
+ * `radius` is stored as given; like Sphere.init (sphere.zig:21) the library clamps it to >= 0. */
+typedef struct rt_sphere {
+    double center[3];
+    double radius;
+    uint32_t material;        /* rt_material_kind */
+    uint32_t reserved;        /* must be 0 */
+    double albedo[3];         /* Lambertian/Metal albedo (material.zig:17,43) */
+    double fuzz;              /* Metal.fuzz (material.zig:45) */
+    double refraction_index;  /* Dielectric.refractionIndex (material.zig:72) */
+} rt_sphere;                  /* 80 bytes */
+
+/* The built Camera (camera.zig:82-103 after CameraBuilder.build camera.zig:300-345) plus the scene
+ * fields render() reads (Scene.interval Scene.zig:21, Scene.seed Scene.zig:19). */
+typedef struct rt_camera {
+    uint32_t image_width;        /* Image.width  (camera.zig:27) */
+    uint32_t image_height;       /* Image.height (camera.zig:28), already trunc(W/ratio), >= 1 */
+    uint32_t samples_per_pixel;  /* Camera.samplesPerPixel (camera.zig:88) */
+    uint32_t bounce_max;         /* Camera.bounceMax (camera.zig:90) */
+    double pixel_samples_scale;  /* Camera.pixelSamplesScale = 1.0/spp (camera.zig:89,284) */
+    double center[3];            /* Camera.center */
+    double pixel0[3];            /* Camera.pixel0 */
+    double du[3];                /* Camera.du */
+    double dv[3];                /* Camera.dv */
+    double defocus_disk_u[3];    /* Camera.defocusDiskU */
+    double defocus_disk_v[3];    /* Camera.defocusDiskV */
+    double defocus_angle;        /* Camera.defocusAngle (degrees; <= 0 disables the disk) */
+    double t_min;                /* Scene.interval.min (1e-3) */
+    double t_max;                /* Scene.interval.max (+inf) */
+    uint64_t seed;               /* Scene.seed (the shim draws one from scene.prng when null) */
+} rt_camera;
+
+/* Options for one render call. */
+typedef enum rt_output_format {
+    RT_OUT_LINEAR_F64 = 0, /* ppm.pixels: linear Color per pixel (camera.zig:137-138) */
+    RT_OUT_RGB8 = 1        /* fused Color.toRgb (color.zig:63-80): 3 bytes per pixel */
+} rt_output_format;
+
+typedef struct rt_options {
+    int32_t n_gpus;        /* 0 => all visible devices; rows are interleaved j mod n_gpus */
+    int32_t device;        /* first device ordinal used */
+    uint32_t pixel_stride; /* LINEAR_F64 only: doubles between pixels; 0 => 3. Zig's
+                              @Vector(3,f64) has stride 4 (32 bytes), so the shim passes 4 */
+    uint32_t output_format;/* rt_output_format */
+    uint64_t* stats_out;   /* optional: [0] = rays traced (world.hit calls), [1] = samples */
+} rt_options;
+
+/* ---- the drop-in: Camera.render() ------------------------------------------------------------ */
+/* Renders the whole image into host memory `out` (row-major, j*W+i).  LINEAR_F64: W*H pixels of
+ * `pixel_stride` doubles (first 3 are r,g,b); RGB8: W*H*3 bytes.  Blocks the calling thread.      */
+int rt_render(const rt_camera* cam, const rt_sphere* spheres, size_t n_spheres,
+              const rt_options* opts, void* out);
+
+/* ---- device-resident path (bench / multi-process drivers) ------------------------------------ */
+typedef struct rt_context rt_context;
+
+int rt_context_create(int device, rt_context** out_ctx);
+int rt_context_destroy(rt_context* ctx);
+/* Uploads the Hittable list to the context's device (once per scene). */
+int rt_context_set_scene(rt_context* ctx, const rt_sphere* spheres, size_t n_spheres);
+/* Renders rows j = row0 + k*row_step, k in [0, n_rows), into DEVICE memory `d_out`
+ * (n_rows*W pixels; LINEAR_F64 stride 3 doubles, or RGB8) on HIP stream `stream` (NULL = default).
+ * Asynchronous: returns after the launch.  `d_stats` (device, 2 x uint64, may be NULL) is
+ * atomically incremented with {rays, samples}. */
+int rt_render_rows_async(rt_context* ctx, const rt_camera* cam, uint32_t output_format,
+                         uint32_t row0, uint32_t row_step, uint32_t n_rows,
+                         void* d_out, void* d_stats, void* stream);
+/* Name of the kernel variant the context launches (for profiling / logs). */
+const char* rt_kernel_name(rt_context* ctx);
+
+/* ---- host mirror of the reference's Scene / CameraBuilder / Color / PPM ---------------------- */
+/* Scene.generateWorld (Scene.zig:48-134) driven by DefaultPrng.init(seed) (Scene.zig:30).
+ * Writes up to `cap` spheres, stores the count in *n (485 for seed 0xdeadbeef).  If `prng_state`
+ * is non-NULL it receives the 4 Xoshiro256++ words after generation (the reference's render()
+ * continues that stream). */
+int rt_scene_final(uint64_t seed, rt_sphere* out, size_t cap, size_t* n, uint64_t* prng_state);
+/* Scene.generateChapter13 (Scene.zig:136-182): 5 spheres, no RNG. */
+int rt_scene_chapter13(rt_sphere* out, size_t cap, size_t* n);
+
+/* CameraBuilder inputs (camera.zig:233-251).  rt_camera_build applies them in the order main.zig
+ * uses (setDefocusAngle, setFocusDist, setViewport, setSamplesPerPixel, setBounceMax): the viewport
+ * is computed from focus_dist (camera.zig:277) and everything else as in build() (:300-345). */
+typedef struct rt_camera_params {
+    uint32_t image_width;
+    uint32_t samples_per_pixel;
+    uint32_t bounce_max;
+    uint32_t reserved;
+    double aspect_ratio;
+    double look_from[3];
+    double look_at[3];
+    double v_up[3];
+    double vfov;           /* degrees */
+    double defocus_angle;  /* degrees */
+    double focus_dist;
+    double t_min, t_max;
+    uint64_t seed;
+} rt_camera_params;
+
+int rt_camera_build(const rt_camera_params* params, rt_camera* out);
+/* Color.toRgb (color.zig:63-76) for n linear pixels with the given stride (doubles). */
+int rt_color_to_rgb8(const double* linear, size_t n_pixels, uint32_t pixel_stride, uint8_t* rgb);
+/* PPM.saveBinary byte stream (ppm.zig:42-60): "P6\nW H\n255\n" + W*H*3 bytes + "\n".
+ * rt_ppm_p6_size gives the byte count; rt_ppm_encode_p6 writes it into `buf`. */
+size_t rt_ppm_p6_size(uint32_t width, uint32_t height);
+int rt_ppm_encode_p6(const uint8_t* rgb, uint32_t width, uint32_t height, uint8_t* buf, size_t cap);
+int rt_ppm_save_p6(const char* path, const uint8_t* rgb, uint32_t width, uint32_t height);
+
+/* Per-(pixel, sample) stream key (DESIGN.md "RNG"); exposed so host tools can reproduce it. */
+uint64_t rt_sample_key(uint64_t seed, uint64_t pixel, uint64_t sample);
+
+const char* rt_last_error(void);
+int rt_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* RT_MI355X_H */
