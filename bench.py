@@ -1,0 +1,219 @@
+#!/usr/bin/env python3
+"""Benchmark: Msamples/s of the per-pixel x per-sample hot path (Camera.render,
+reference src/camera.zig:123-145) on the final random-sphere scene — BASELINE.json config 4:
+1200x800, 500 spp, depth 50, 485 spheres (seed 0xdeadbeef), rows interleaved over N GPUs.
+
+    python bench.py --gpus N --steps K --warmup W
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+A step = one full frame: every rank renders its rows (HIP kernel via the C ABI, inputs resident in
+HBM) and the rows are gathered to rank 0 over RCCL.  The image is fixed, so N>1 is strong scaling.
+Rank 0 prints ONE JSON line.  `roofline` is the dominant kernel's FP64-VALU roofline (17 FLOPs per
+ray-sphere candidate test x spheres x rays); `cpu_baseline` times the oracle's
+sequential-stream port of the reference (single thread — the reference's single RNG stream is
+inherently sequential) on a bounded sample of the same frame.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "raytracing-with-zig_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+import rtzig  # noqa: E402
+from rtzig import dist as rdist  # noqa: E402
+
+METRIC = "Msamples/sec (pixels×spp/s) on final-render scene; achieved HBM GB/s vs peak"
+FP64_VALU_PEAK_TFLOPS = 78.6   # MI355X vector FP64 (spec), = unpacked FP32 vector rate
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E (spec), MI355X_MICROARCH.md
+FLOPS_PER_TEST = 17            # oc(3) + h(5) + |oc|^2(5) + -r^2(1) + h^2-a*c(3), SURVEY §8(d)
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(width, aspect, cpu_spp):
+    """Oracle A (reference port, sequential Xoshiro stream, one thread) on a bounded sample:
+    the full config-4 frame at `cpu_spp` samples per pixel."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import ctypes as C
+
+    from oracle_lib import Oracle
+    from rtzig.abi import D3, RtCameraParams
+    o = Oracle()
+    spheres, state = o.scene_final(0xDEADBEEF)
+    p = RtCameraParams(image_width=width, samples_per_pixel=cpu_spp, bounce_max=50,
+                       aspect_ratio=aspect, look_from=D3(13, 2, 3), look_at=D3(0, 0, 0),
+                       v_up=D3(0, 1, 0), vfov=20, defocus_angle=0.6, focus_dist=10,
+                       t_min=1e-3, t_max=float("inf"), seed=0xDEADBEEF)
+    cam = o.camera_build(p)
+    t0 = time.perf_counter()
+    _, rays = o.render_a(cam, spheres, state)
+    dt = time.perf_counter() - t0
+    n = cam.image_width * cam.image_height * cpu_spp
+    return {"value": round(n / dt / 1e6, 4), "unit": "Msamples/s", "cores": 1, "kind": "port",
+            "sample": f"oracle A (C restatement of the Zig reference, sequential RNG stream, -O3) "
+                      f"full {cam.image_width}x{cam.image_height} frame at {cpu_spp} spp "
+                      f"({n} samples, {rays} rays) in {dt:.2f} s"}
+
+
+def pmc_traffic(workload):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary (profiles/pmc_traffic.json,
+    written by tools/pmc_traffic.py from separate FETCH_SIZE / WRITE_SIZE passes), or None."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        d = json.load(open(path))
+    except (OSError, ValueError):
+        return None
+    if d.get("workload") != workload:
+        return None
+    return d.get("hbm_bytes_per_launch")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--width", type=int, default=1200)
+    ap.add_argument("--aspect", type=float, default=1.5)
+    ap.add_argument("--spp", type=int, default=500)
+    ap.add_argument("--output", choices=["linear", "rgb8"], default="linear")
+    ap.add_argument("--cpu-spp", type=int, default=4, help="spp of the bounded CPU-baseline sample")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus != world and world > 1:
+        log(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+
+    t_init = time.perf_counter()
+    cam = rtzig.final_scene_camera(width=args.width, aspect_ratio=args.aspect, spp=args.spp)
+    H, W, spp = cam.height, cam.width, args.spp
+    n_spheres = len(cam.scene.world)
+    row0, step, n_rows = rdist.rank_rows(H, rank, world)
+    R = rdist.rows_per_rank(H, world)
+    renderer = rtzig.DeviceRenderer(local)
+    renderer.set_scene(cam.scene.world)
+    if args.output == "linear":
+        out = torch.zeros((R, W, 3), dtype=torch.float64, device=dev)
+    else:
+        out = torch.zeros((R, W, 3), dtype=torch.uint8, device=dev)
+    stats = torch.zeros(2, dtype=torch.int64, device=dev)
+    stream = torch.cuda.current_stream()
+    torch.cuda.synchronize()
+    init_ms = (time.perf_counter() - t_init) * 1e3
+
+    def frame(stats_ptr=None, events=None):
+        if events is not None:
+            events[0].record(stream)
+        if n_rows:
+            renderer.render_rows_async(cam.cam, out.data_ptr(), row0=row0, row_step=step,
+                                       n_rows=n_rows, output=args.output, d_stats_ptr=stats_ptr,
+                                       stream_ptr=stream.cuda_stream)
+        if events is not None:
+            events[1].record(stream)
+        return rdist.gather_image(out, H, rank, world)
+
+    for _ in range(args.warmup):
+        frame()
+    stats.zero_()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(args.steps)]
+
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    img = None
+    for k in range(args.steps):
+        img = frame(stats.data_ptr(), evs[k])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed_max = float(t.item())
+    kernel_ms = [a.elapsed_time(b) for a, b in evs]
+    st = stats.cpu().tolist()
+    rays_per_launch = st[0] / max(1, args.steps)
+    samples_per_launch = st[1] / max(1, args.steps)
+
+    if rank == 0:
+        total_samples = W * H * spp * args.steps
+        value = total_samples / elapsed_max / 1e6
+        k_avg_s = float(np.mean(kernel_ms)) / 1e3
+        flops = FLOPS_PER_TEST * n_spheres * rays_per_launch
+        achieved_tf = flops / k_avg_s / 1e12
+        out_bytes = n_rows * W * (24 if args.output == "linear" else 3)
+        alg_bytes = out_bytes + n_spheres * (32 + 64)
+        workload = f"final-render {W}x{H} {spp}spp depth50 ({n_spheres} spheres)"
+        traffic = pmc_traffic(workload)
+        assert img is not None and img.shape[0] == H
+        res = {
+            "metric": METRIC,
+            "value": round(value, 3),
+            "unit": "Msamples/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed_max / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic: final random-sphere scene generated in-process (Scene.generateWorld, "
+                    "seed 0xdeadbeef), main.zig camera preset",
+            "config": {"workload": workload, "width": W, "height": H, "spp": spp, "depth": 50,
+                       "spheres": n_spheres, "output": args.output,
+                       "parallelism": f"rows interleaved over {world} GPU(s), RCCL gather to rank 0"},
+            "roofline": {
+                "bound": "valu",
+                "kernel": renderer.kernel_name(),
+                "achieved": round(achieved_tf, 3),
+                "peak": FP64_VALU_PEAK_TFLOPS,
+                "unit": "TFLOP/s",
+                "frac": round(achieved_tf / FP64_VALU_PEAK_TFLOPS, 4),
+                "traffic": traffic,
+                "work": f"{FLOPS_PER_TEST} FLOP x {n_spheres} spheres x {rays_per_launch:.0f} rays "
+                        f"per launch (rank 0, {n_rows} rows)",
+                "kernel_ms_avg": round(k_avg_s * 1e3, 3),
+            },
+            "hbm": {
+                "algorithmic_bytes_per_launch": alg_bytes,
+                "achieved_GBps": round(alg_bytes / k_avg_s / 1e9, 3),
+                "peak_GBps": HBM_PEAK_GBS,
+                "frac": round(alg_bytes / k_avg_s / 1e9 / HBM_PEAK_GBS, 6),
+            },
+            "rays_per_sample": round(rays_per_launch / max(1, samples_per_launch), 4),
+            "fixed_costs_ms": {"context_and_scene_upload": round(init_ms, 2)},
+            "cpu_baseline": None,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            res["cpu_baseline"] = cpu_baseline(W, args.aspect, args.cpu_spp)
+            res["speedup_vs_cpu_baseline"] = round(value / res["cpu_baseline"]["value"], 1)
+        print(json.dumps(res), flush=True)
+    renderer.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

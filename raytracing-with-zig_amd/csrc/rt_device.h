@@ -1,0 +1,161 @@
+// rt_device.h — device-side math, RNG and material scatter for the MI355X path tracer (gfx950).
+//
+// Arithmetic contract (DESIGN.md "Parity"): every f64 operation rounds where the reference's does.
+// The reference is Zig 0.14 in strict float mode: no FMA contraction, @reduce(.Add) evaluated as
+// (x+y)+z, correctly rounded @sqrt and division.  hipcc defaults to -ffp-contract=fast for HIP, so
+// this header pins contraction off with a pragma in addition to the build flag.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#pragma clang fp contract(off)
+
+namespace rtk {
+
+// ------------------------------------------------------------------------------------------------
+// Vec3 (vec.zig:5-136)
+// ------------------------------------------------------------------------------------------------
+struct v3 {
+    double x, y, z;
+};
+
+__device__ __forceinline__ v3 mk(double x, double y, double z) { return v3{x, y, z}; }
+__device__ __forceinline__ v3 operator+(v3 a, v3 b) { return v3{a.x + b.x, a.y + b.y, a.z + b.z}; }
+__device__ __forceinline__ v3 operator-(v3 a, v3 b) { return v3{a.x - b.x, a.y - b.y, a.z - b.z}; }
+__device__ __forceinline__ v3 operator*(v3 a, v3 b) { return v3{a.x * b.x, a.y * b.y, a.z * b.z}; }
+__device__ __forceinline__ v3 operator-(v3 a) { return v3{-a.x, -a.y, -a.z}; }
+// Vec.mulScalar (vec.zig:35)
+__device__ __forceinline__ v3 muls(v3 a, double s) { return v3{a.x * s, a.y * s, a.z * s}; }
+// Vec.dot / lenSquared: @reduce(.Add) is the ordered (x+y)+z (vec.zig:51,114)
+__device__ __forceinline__ double dot(v3 a, v3 b) { return (a.x * b.x + a.y * b.y) + a.z * b.z; }
+__device__ __forceinline__ double len_sq(v3 a) { return (a.x * a.x + a.y * a.y) + a.z * a.z; }
+// Vec.unit = divScalar(v, len) = v * (1/len) (vec.zig:39-45,126)
+__device__ __forceinline__ v3 unit(v3 a) { return muls(a, 1.0 / __builtin_sqrt(len_sq(a))); }
+// Vec.nearZero: all(v < 1e-8) with no abs (vec.zig:26-29)
+__device__ __forceinline__ bool near_zero(v3 v) { return v.x < 1e-8 && v.y < 1e-8 && v.z < 1e-8; }
+// Vec.reflect = v - (n * dot(v,n)) * 2 (vec.zig:103-105)
+__device__ __forceinline__ v3 reflect(v3 v, v3 n) { return v - muls(muls(n, dot(v, n)), 2.0); }
+// Vec.refract (vec.zig:107-112)
+__device__ __forceinline__ v3 refract(v3 v, v3 n, double eta) {
+    const double cos_t = __builtin_fmin(dot(-v, n), 1.0);
+    const v3 r_perp = muls(v + muls(n, cos_t), eta);
+    const v3 r_par = muls(n, -__builtin_sqrt(__builtin_fabs(1.0 - len_sq(r_perp))));
+    return r_perp + r_par;
+}
+
+// ------------------------------------------------------------------------------------------------
+// RNG.  The reference draws from ONE Xoshiro256++ stream (std.Random.DefaultPrng, Scene.zig:30).
+// Here every (pixel, sample) owns a Xoshiro256++ stream seeded through SplitMix64 exactly like
+// DefaultPrng.init, from the key rt_sample_key(seed, pixel, sample) — counter-based, so any
+// partition of the image over lanes/GPUs draws the same numbers.
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t rotl64(uint64_t x, int k) { return (x << k) | (x >> (64 - k)); }
+
+// SplitMix64.next (zig std/Random/SplitMix64.zig)
+__device__ __forceinline__ uint64_t splitmix_next(uint64_t& s) {
+    s += 0x9e3779b97f4a7c15ULL;
+    uint64_t z = s;
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
+    return z ^ (z >> 31);
+}
+__host__ __device__ __forceinline__ uint64_t sm_mix_hd(uint64_t x) {
+    x += 0x9e3779b97f4a7c15ULL;
+    uint64_t z = x;
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
+    return z ^ (z >> 31);
+}
+
+struct Rng {
+    uint64_t s0, s1, s2, s3;
+
+    // DefaultPrng.init(key): Xoshiro256.seed via SplitMix64 (zig std/Random/Xoshiro256.zig)
+    __device__ __forceinline__ void seed(uint64_t key) {
+        uint64_t sm = key;
+        s0 = splitmix_next(sm);
+        s1 = splitmix_next(sm);
+        s2 = splitmix_next(sm);
+        s3 = splitmix_next(sm);
+    }
+    // Xoshiro256.next
+    __device__ __forceinline__ uint64_t next() {
+        const uint64_t r = rotl64(s0 + s3, 23) + s0;
+        const uint64_t t = s1 << 17;
+        s2 ^= s0;
+        s3 ^= s1;
+        s1 ^= s2;
+        s0 ^= s3;
+        s2 ^= t;
+        s3 = rotl64(s3, 45);
+        return r;
+    }
+    // Random.float(f64) (zig std/Random.zig): mantissa = low 52 bits, exponent from leading zeros;
+    // >= 12 leading zeros (p = 1/4096) pulls further draws.
+    __device__ __forceinline__ double uniform() {
+        const uint64_t rnd = next();
+        uint64_t lz = rnd ? (uint64_t)__builtin_clzll(rnd) : 64;
+        if (__builtin_expect(lz >= 12, 0)) {
+            lz = 12;
+            for (;;) {
+                const uint64_t w = next();
+                const uint64_t add = w ? (uint64_t)__builtin_clzll(w) : 64;
+                lz += add;
+                if (add != 64) break;
+                if (lz >= 1022) { lz = 1022; break; }
+            }
+        }
+        const uint64_t bits = ((1022 - lz) << 52) | (rnd & ((1ULL << 52) - 1));
+        return __builtin_bit_cast(double, bits);
+    }
+    // util.randomDoubleRange (util.zig:20-22)
+    __device__ __forceinline__ double range(double mn, double mx) { return mn + (mx - mn) * uniform(); }
+};
+
+// key(seed, pixel, sample) = mix(mix(seed) ^ (pixel << 32 | sample)); seed_mix = mix(seed) is
+// hoisted to the host.  For a fixed seed the map (pixel, sample) -> key is a bijection.
+__device__ __forceinline__ uint64_t sample_key(uint64_t seed_mix, uint64_t pixel, uint32_t sample) {
+    return sm_mix_hd(seed_mix ^ ((pixel << 32) | (uint64_t)sample));
+}
+
+// Vec.randomUnitVec (vec.zig:71-80): rejection in the cube, then TRUE division by the length.
+__device__ __forceinline__ v3 random_unit_vec(Rng& g) {
+    for (;;) {
+        const double x = g.range(-1, 1);
+        const double y = g.range(-1, 1);
+        const double z = g.range(-1, 1);
+        const double ls = (x * x + y * y) + z * z;
+        if (1e-160 < ls && ls <= 1) {
+            const double l = __builtin_sqrt(ls);
+            return v3{x / l, y / l, z / l};
+        }
+    }
+}
+
+// Vec.randomInUnitDisk (vec.zig:82-92)
+__device__ __forceinline__ v3 random_in_unit_disk(Rng& g) {
+    for (;;) {
+        const double x = g.range(-1, 1);
+        const double y = g.range(-1, 1);
+        if ((x * x + y * y) + 0.0 * 0.0 < 1) return v3{x, y, 0.0};
+    }
+}
+
+// std.math.pow(f64, x, 5) for x in [0, 2] (frexp + repeated squaring == x*((x*x)*(x*x)))
+__device__ __forceinline__ double zig_pow5(double x) {
+    if (x == 1.0) return 1.0;
+    if (x == 0.0) return x;
+    const double x2 = x * x;
+    const double x4 = x2 * x2;
+    return x * x4;
+}
+
+// Color.toRgb for one channel (color.zig:63-80): sqrt gamma, clamp [0, 0.999], trunc(256*x)
+__device__ __forceinline__ uint8_t to_byte(double lin) {
+    double g = lin > 0 ? __builtin_sqrt(lin) : 0.0;
+    g = g < 0.0 ? 0.0 : (g > 0.999 ? 0.999 : g);
+    return (uint8_t)(int)(256.0 * g);
+}
+
+}  // namespace rtk

@@ -1,0 +1,307 @@
+// rt_runtime.cpp — device runtime behind the C ABI: contexts, scene upload, launches, and the
+// blocking multi-GPU rt_render() that replaces Camera.render (camera.zig:123-145).
+//
+// Multi-GPU inside one call: one host thread drives every device asynchronously (one stream per
+// GPU).  Rows are interleaved (row j on device j mod G) so sky-heavy and ground-heavy rows spread
+// evenly; each device renders its rows into its own buffer, copies them back, and the host
+// un-interleaves them into the caller's framebuffer.  Because the RNG is keyed by the GLOBAL pixel
+// index, the image is bit-identical for any device count.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/rt.h"
+#include "rt_device.h"
+#include "rt_kernel.h"
+
+void rt_set_last_error(const std::string& msg);
+
+struct rt_context {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    rtk::GeoRec* d_geo = nullptr;
+    rtk::MatRec* d_mat = nullptr;
+    uint32_t n_spheres = 0;
+    uint32_t capacity = 0;
+    const char* last_kernel = "render_kernel";
+};
+
+namespace {
+
+int hip_fail(hipError_t e, const char* what) {
+    rt_set_last_error(std::string(what) + ": " + hipGetErrorString(e));
+    return e == hipErrorNoDevice || e == hipErrorInvalidDevice ? RT_ERR_NO_DEVICE : RT_ERR_HIP;
+}
+
+#define HIP_CHECK(expr)                                  \
+    do {                                                 \
+        hipError_t _e = (expr);                          \
+        if (_e != hipSuccess) return hip_fail(_e, #expr); \
+    } while (0)
+
+int validate_camera(const rt_camera* c) {
+    if (!c) { rt_set_last_error("null camera"); return RT_ERR_INVALID; }
+    if (c->image_width == 0 || c->image_height == 0) {
+        rt_set_last_error("image_width and image_height must be > 0");
+        return RT_ERR_INVALID;
+    }
+    if (c->samples_per_pixel == 0) {
+        rt_set_last_error("samples_per_pixel must be > 0");
+        return RT_ERR_INVALID;
+    }
+    if ((uint64_t)c->image_width * c->image_height > (1ULL << 32)) {
+        rt_set_last_error("image larger than 2^32 pixels");
+        return RT_ERR_INVALID;
+    }
+    return RT_OK;
+}
+
+int validate_spheres(const rt_sphere* s, size_t n) {
+    if (n == 0 || !s) { rt_set_last_error("empty sphere list"); return RT_ERR_INVALID; }
+    if (n > (1u << 24)) { rt_set_last_error("too many spheres"); return RT_ERR_CAPACITY; }
+    for (size_t k = 0; k < n; k++) {
+        if (s[k].material > RT_DIELECTRIC) {
+            rt_set_last_error("sphere " + std::to_string(k) + ": unknown material kind");
+            return RT_ERR_INVALID;
+        }
+        if (std::isnan(s[k].radius)) {
+            rt_set_last_error("sphere " + std::to_string(k) + ": radius is NaN");
+            return RT_ERR_INVALID;
+        }
+    }
+    return RT_OK;
+}
+
+rtk::KernelParams make_params(const rt_camera* c, uint32_t fmt, uint32_t row0, uint32_t row_step,
+                              uint32_t n_rows, uint32_t n_spheres) {
+    rtk::KernelParams p;
+    std::memset(&p, 0, sizeof p);
+    p.width = c->image_width;
+    p.height = c->image_height;
+    p.spp = c->samples_per_pixel;
+    p.bounce_max = c->bounce_max;
+    p.scale = c->pixel_samples_scale;
+    for (int k = 0; k < 3; k++) {
+        p.center[k] = c->center[k];
+        p.pixel0[k] = c->pixel0[k];
+        p.du[k] = c->du[k];
+        p.dv[k] = c->dv[k];
+        p.ddu[k] = c->defocus_disk_u[k];
+        p.ddv[k] = c->defocus_disk_v[k];
+    }
+    p.defocus_angle = c->defocus_angle;
+    p.t_min = c->t_min;
+    p.t_max = c->t_max;
+    p.seed_mix = rtk::sm_mix_hd(c->seed);
+    p.row0 = row0;
+    p.row_step = row_step;
+    p.n_rows = n_rows;
+    p.n_spheres = n_spheres;
+    p.out_format = fmt;
+    return p;
+}
+
+}  // namespace
+
+extern "C" {
+
+int rt_context_create(int device, rt_context** out_ctx) {
+    if (!out_ctx) { rt_set_last_error("null out_ctx"); return RT_ERR_INVALID; }
+    int count = 0;
+    HIP_CHECK(hipGetDeviceCount(&count));
+    if (device < 0 || device >= count) {
+        rt_set_last_error("device ordinal " + std::to_string(device) + " out of range (" +
+                          std::to_string(count) + " visible)");
+        return RT_ERR_NO_DEVICE;
+    }
+    HIP_CHECK(hipSetDevice(device));
+    hipDeviceProp_t prop;
+    HIP_CHECK(hipGetDeviceProperties(&prop, device));
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+        rt_set_last_error(std::string("device is ") + prop.gcnArchName + ", library built for gfx950");
+        return RT_ERR_NO_DEVICE;
+    }
+    auto* ctx = new rt_context;
+    ctx->device = device;
+    hipError_t e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+        delete ctx;
+        return hip_fail(e, "hipStreamCreate");
+    }
+    *out_ctx = ctx;
+    return RT_OK;
+}
+
+int rt_context_destroy(rt_context* ctx) {
+    if (!ctx) return RT_OK;
+    (void)hipSetDevice(ctx->device);
+    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    (void)hipFree(ctx->d_geo);
+    (void)hipFree(ctx->d_mat);
+    if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+    return RT_OK;
+}
+
+int rt_context_set_scene(rt_context* ctx, const rt_sphere* spheres, size_t n) {
+    if (!ctx) { rt_set_last_error("null context"); return RT_ERR_INVALID; }
+    int rc = validate_spheres(spheres, n);
+    if (rc) return rc;
+    HIP_CHECK(hipSetDevice(ctx->device));
+    std::vector<rtk::GeoRec> geo(n);
+    std::vector<rtk::MatRec> mat(n);
+    for (size_t k = 0; k < n; k++) {
+        const double r = spheres[k].radius > 0 ? spheres[k].radius : 0.0;  // sphere.zig:21
+        geo[k].cx = spheres[k].center[0];
+        geo[k].cy = spheres[k].center[1];
+        geo[k].cz = spheres[k].center[2];
+        geo[k].r2 = r * r;
+        std::memset(&mat[k], 0, sizeof mat[k]);
+        for (int c = 0; c < 3; c++) mat[k].albedo[c] = spheres[k].albedo[c];
+        mat[k].fuzz = spheres[k].fuzz;
+        mat[k].ior = spheres[k].refraction_index;
+        mat[k].inv_r = 1.0 / r;
+        mat[k].kind = spheres[k].material;
+    }
+    if (n > ctx->capacity) {
+        (void)hipFree(ctx->d_geo);
+        (void)hipFree(ctx->d_mat);
+        ctx->d_geo = nullptr;
+        ctx->d_mat = nullptr;
+        ctx->capacity = 0;
+        HIP_CHECK(hipMalloc(&ctx->d_geo, n * sizeof(rtk::GeoRec)));
+        HIP_CHECK(hipMalloc(&ctx->d_mat, n * sizeof(rtk::MatRec)));
+        ctx->capacity = (uint32_t)n;
+    }
+    HIP_CHECK(hipMemcpyAsync(ctx->d_geo, geo.data(), n * sizeof(rtk::GeoRec), hipMemcpyHostToDevice, ctx->stream));
+    HIP_CHECK(hipMemcpyAsync(ctx->d_mat, mat.data(), n * sizeof(rtk::MatRec), hipMemcpyHostToDevice, ctx->stream));
+    HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    ctx->n_spheres = (uint32_t)n;
+    return RT_OK;
+}
+
+int rt_render_rows_async(rt_context* ctx, const rt_camera* cam, uint32_t output_format, uint32_t row0,
+                         uint32_t row_step, uint32_t n_rows, void* d_out, void* d_stats, void* stream) {
+    if (!ctx) { rt_set_last_error("null context"); return RT_ERR_INVALID; }
+    int rc = validate_camera(cam);
+    if (rc) return rc;
+    if (ctx->n_spheres == 0) { rt_set_last_error("no scene uploaded"); return RT_ERR_INVALID; }
+    if (output_format > RT_OUT_RGB8) { rt_set_last_error("bad output_format"); return RT_ERR_INVALID; }
+    if (n_rows == 0) return RT_OK;
+    if (!d_out) { rt_set_last_error("null output"); return RT_ERR_INVALID; }
+    if (row_step == 0) row_step = 1;
+    const uint64_t last_row = (uint64_t)row0 + (uint64_t)(n_rows - 1) * row_step;
+    if (last_row >= cam->image_height) {
+        rt_set_last_error("row range exceeds image_height");
+        return RT_ERR_INVALID;
+    }
+    HIP_CHECK(hipSetDevice(ctx->device));
+    const rtk::KernelParams p = make_params(cam, output_format, row0, row_step, n_rows, ctx->n_spheres);
+    hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+    HIP_CHECK(rtk_launch_render(&p, ctx->d_geo, ctx->d_mat, d_out, d_stats, s, &ctx->last_kernel));
+    return RT_OK;
+}
+
+const char* rt_kernel_name(rt_context* ctx) { return ctx ? ctx->last_kernel : "render_kernel"; }
+
+int rt_render(const rt_camera* cam, const rt_sphere* spheres, size_t n, const rt_options* opts, void* out) {
+    int rc = validate_camera(cam);
+    if (rc) return rc;
+    rc = validate_spheres(spheres, n);
+    if (rc) return rc;
+    if (!out) { rt_set_last_error("null output"); return RT_ERR_INVALID; }
+    rt_options o{};
+    if (opts) o = *opts;
+    if (o.output_format > RT_OUT_RGB8) { rt_set_last_error("bad output_format"); return RT_ERR_INVALID; }
+    const uint32_t stride = o.pixel_stride ? o.pixel_stride : 3;
+    if (o.output_format == RT_OUT_LINEAR_F64 && stride < 3) {
+        rt_set_last_error("pixel_stride must be >= 3");
+        return RT_ERR_INVALID;
+    }
+    int count = 0;
+    HIP_CHECK(hipGetDeviceCount(&count));
+    if (count <= 0) { rt_set_last_error("no HIP device"); return RT_ERR_NO_DEVICE; }
+    const int first = o.device;
+    int G = o.n_gpus > 0 ? o.n_gpus : count - first;
+    if (first < 0 || first + G > count || G <= 0) {
+        rt_set_last_error("requested devices not available");
+        return RT_ERR_NO_DEVICE;
+    }
+    const uint32_t W = cam->image_width, H = cam->image_height;
+    G = std::min<int>(G, (int)H);
+    const size_t px_bytes = o.output_format == RT_OUT_LINEAR_F64 ? 3 * sizeof(double) : 3;
+
+    struct Dev {
+        rt_context* ctx = nullptr;
+        void* d_out = nullptr;
+        uint64_t* d_stats = nullptr;
+        std::vector<uint8_t> host;
+        uint32_t n_rows = 0;
+    };
+    std::vector<Dev> devs(G);
+    auto cleanup = [&]() {
+        for (auto& d : devs) {
+            if (!d.ctx) continue;
+            (void)hipSetDevice(d.ctx->device);
+            (void)hipFree(d.d_out);
+            (void)hipFree(d.d_stats);
+            rt_context_destroy(d.ctx);
+        }
+    };
+    for (int g = 0; g < G; g++) {
+        Dev& d = devs[g];
+        rc = rt_context_create(first + g, &d.ctx);
+        if (!rc) rc = rt_context_set_scene(d.ctx, spheres, n);
+        if (rc) { cleanup(); return rc; }
+        d.n_rows = (H - (uint32_t)g + (uint32_t)G - 1) / (uint32_t)G;
+        const size_t bytes = (size_t)d.n_rows * W * px_bytes;
+        hipError_t e = hipMalloc(&d.d_out, bytes ? bytes : 1);
+        if (e == hipSuccess) e = hipMalloc((void**)&d.d_stats, 2 * sizeof(uint64_t));
+        if (e == hipSuccess) e = hipMemsetAsync(d.d_stats, 0, 2 * sizeof(uint64_t), d.ctx->stream);
+        if (e != hipSuccess) { cleanup(); return hip_fail(e, "hipMalloc"); }
+        rc = rt_render_rows_async(d.ctx, cam, o.output_format, (uint32_t)g, (uint32_t)G, d.n_rows,
+                                  d.d_out, d.d_stats, nullptr);
+        if (rc) { cleanup(); return rc; }
+    }
+    uint64_t stats[2] = {0, 0};
+    for (int g = 0; g < G; g++) {
+        Dev& d = devs[g];
+        (void)hipSetDevice(d.ctx->device);
+        d.host.resize((size_t)d.n_rows * W * px_bytes);
+        uint64_t st[2] = {0, 0};
+        hipError_t e = hipMemcpyAsync(d.host.data(), d.d_out, d.host.size(), hipMemcpyDeviceToHost, d.ctx->stream);
+        if (e == hipSuccess) e = hipMemcpyAsync(st, d.d_stats, sizeof st, hipMemcpyDeviceToHost, d.ctx->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(d.ctx->stream);
+        if (e != hipSuccess) { cleanup(); return hip_fail(e, "render/copy-back"); }
+        stats[0] += st[0];
+        stats[1] += st[1];
+        // un-interleave rows j = g + k*G into the caller's framebuffer
+        for (uint32_t k = 0; k < d.n_rows; k++) {
+            const uint32_t j = (uint32_t)g + k * (uint32_t)G;
+            if (o.output_format == RT_OUT_RGB8) {
+                std::memcpy((uint8_t*)out + (size_t)j * W * 3, d.host.data() + (size_t)k * W * 3, (size_t)W * 3);
+            } else {
+                const double* src = (const double*)d.host.data() + (size_t)k * W * 3;
+                double* dst = (double*)out + (size_t)j * W * stride;
+                if (stride == 3) {
+                    std::memcpy(dst, src, (size_t)W * 3 * sizeof(double));
+                } else {
+                    for (uint32_t i = 0; i < W; i++)
+                        for (int c = 0; c < 3; c++) dst[(size_t)i * stride + c] = src[3 * (size_t)i + c];
+                }
+            }
+        }
+    }
+    cleanup();
+    if (o.stats_out) {
+        o.stats_out[0] = stats[0];
+        o.stats_out[1] = stats[1];
+    }
+    return RT_OK;
+}
+
+}  // extern "C"

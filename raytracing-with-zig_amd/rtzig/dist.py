@@ -1,0 +1,41 @@
+"""Row-interleaved partition of one image over ranks + the final gather to rank 0.
+
+SURVEY §8(e): pixels are independent, so rendering needs no exchange; row j goes to rank
+j mod world (interleaving spreads cheap sky rows and expensive ground rows evenly).  The one
+collective is the final gather of every rank's rows to rank 0 (RCCL over xGMI with the "nccl"
+backend on ROCm; gloo on CPU in tests).  The RNG is keyed by the global pixel index, so the
+gathered image is bit-identical for any world size.
+"""
+import torch
+import torch.distributed as dist
+
+
+def rows_per_rank(height, world):
+    """Padded per-rank row count R = ceil(H / world); rank r owns rows r, r+world, ..."""
+    return (height + world - 1) // world
+
+
+def rank_rows(height, rank, world):
+    """(row0, row_step, n_rows) for this rank's interleaved rows."""
+    n = (height - rank + world - 1) // world if rank < height else 0
+    return rank, world, n
+
+
+def assemble(gathered, height):
+    """gathered: (world, R, W, C) with slot [r][k] = row r + k*world -> (H, W, C) image."""
+    world, R = gathered.shape[0], gathered.shape[1]
+    img = gathered.transpose(0, 1).reshape(R * world, *gathered.shape[2:])
+    return img[:height]
+
+
+def gather_image(local, height, rank, world, group=None):
+    """local: (R, W, C) padded rows of this rank (rows beyond its n_rows are ignored).
+    Returns the (H, W, C) image on rank 0 and None elsewhere."""
+    if world == 1:
+        return local[:height]
+    if rank == 0:
+        bufs = [torch.empty_like(local) for _ in range(world)]
+        dist.gather(local, gather_list=bufs, dst=0, group=group)
+        return assemble(torch.stack(bufs), height)
+    dist.gather(local, dst=0, group=group)
+    return None

@@ -1,0 +1,92 @@
+"""Loader for librtzig.so (the HIP path tracer + C ABI of include/rt.h).
+
+The product path has NO fallback: if the shared library is missing this module raises, and every
+render call goes through the HIP kernel on a gfx950 device (rt_render / rt_render_rows_async).
+"""
+import ctypes as C
+import os
+
+from .abi import RtCamera, RtCameraParams, RtOptions, RtSphere
+
+PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(PKG_DIR, "librtzig.so")
+
+# Every symbol include/rt.h declares (tests/test_abi.py checks the header against this list).
+EXPORTED = [
+    "rt_render",
+    "rt_context_create",
+    "rt_context_destroy",
+    "rt_context_set_scene",
+    "rt_render_rows_async",
+    "rt_kernel_name",
+    "rt_scene_final",
+    "rt_scene_chapter13",
+    "rt_camera_build",
+    "rt_color_to_rgb8",
+    "rt_ppm_p6_size",
+    "rt_ppm_encode_p6",
+    "rt_ppm_save_p6",
+    "rt_sample_key",
+    "rt_last_error",
+    "rt_abi_version",
+]
+
+
+class RtError(RuntimeError):
+    def __init__(self, fn, code, msg):
+        super().__init__(f"{fn} failed ({code}): {msg}")
+        self.code = code
+
+
+_lib = None
+
+
+def _declare(lib):
+    P = C.POINTER
+    vp = C.c_void_p
+    sigs = {
+        "rt_render": (C.c_int, [P(RtCamera), P(RtSphere), C.c_size_t, P(RtOptions), vp]),
+        "rt_context_create": (C.c_int, [C.c_int, P(vp)]),
+        "rt_context_destroy": (C.c_int, [vp]),
+        "rt_context_set_scene": (C.c_int, [vp, P(RtSphere), C.c_size_t]),
+        "rt_render_rows_async": (C.c_int, [vp, P(RtCamera), C.c_uint32, C.c_uint32, C.c_uint32,
+                                           C.c_uint32, vp, vp, vp]),
+        "rt_kernel_name": (C.c_char_p, [vp]),
+        "rt_scene_final": (C.c_int, [C.c_uint64, P(RtSphere), C.c_size_t, P(C.c_size_t),
+                                     P(C.c_uint64)]),
+        "rt_scene_chapter13": (C.c_int, [P(RtSphere), C.c_size_t, P(C.c_size_t)]),
+        "rt_camera_build": (C.c_int, [P(RtCameraParams), P(RtCamera)]),
+        "rt_color_to_rgb8": (C.c_int, [P(C.c_double), C.c_size_t, C.c_uint32, P(C.c_uint8)]),
+        "rt_ppm_p6_size": (C.c_size_t, [C.c_uint32, C.c_uint32]),
+        "rt_ppm_encode_p6": (C.c_int, [P(C.c_uint8), C.c_uint32, C.c_uint32, P(C.c_uint8),
+                                       C.c_size_t]),
+        "rt_ppm_save_p6": (C.c_int, [C.c_char_p, P(C.c_uint8), C.c_uint32, C.c_uint32]),
+        "rt_sample_key": (C.c_uint64, [C.c_uint64, C.c_uint64, C.c_uint64]),
+        "rt_last_error": (C.c_char_p, []),
+        "rt_abi_version": (C.c_int, []),
+    }
+    for name, (res, args) in sigs.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+
+
+def load():
+    """Load librtzig.so (raises if it has not been built — there is no CPU fallback)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(
+                f"{LIB_PATH} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+                "(make -C raytracing-with-zig_amd/csrc)")
+        lib = C.CDLL(LIB_PATH)
+        _declare(lib)
+        _lib = lib
+    return _lib
+
+
+def check(fn_name, rc):
+    if rc != 0:
+        msg = load().rt_last_error()
+        raise RtError(fn_name, rc, msg.decode() if msg else "")
+    return rc
