@@ -201,7 +201,7 @@ int rt_render_rows_async(rt_context* ctx, const rt_camera* cam, uint32_t output_
     }
     HIP_CHECK(hipSetDevice(ctx->device));
     const rtk::KernelParams p = make_params(cam, output_format, row0, row_step, n_rows, ctx->n_spheres);
-    hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+    hipStream_t s = (hipStream_t)stream;  // NULL = the HIP null stream, like torch's default stream
     HIP_CHECK(rtk_launch_render(&p, ctx->d_geo, ctx->d_mat, d_out, d_stats, s, &ctx->last_kernel));
     return RT_OK;
 }
@@ -264,7 +264,7 @@ int rt_render(const rt_camera* cam, const rt_sphere* spheres, size_t n, const rt
         if (e == hipSuccess) e = hipMemsetAsync(d.d_stats, 0, 2 * sizeof(uint64_t), d.ctx->stream);
         if (e != hipSuccess) { cleanup(); return hip_fail(e, "hipMalloc"); }
         rc = rt_render_rows_async(d.ctx, cam, o.output_format, (uint32_t)g, (uint32_t)G, d.n_rows,
-                                  d.d_out, d.d_stats, nullptr);
+                                  d.d_out, d.d_stats, d.ctx->stream);
         if (rc) { cleanup(); return rc; }
     }
     uint64_t stats[2] = {0, 0};
