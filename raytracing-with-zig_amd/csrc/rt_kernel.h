@@ -1,4 +1,4 @@
-// rt_kernel.h — device data layout shared by the kernel (rt_kernel.hip) and the host runtime.
+// rt_kernel.h — device data layout shared by the kernels (rt_kernel.hip) and the host runtime.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -6,8 +6,9 @@
 
 namespace rtk {
 
-constexpr int kBlock = 256;               // 4 waves of 64 lanes
-constexpr uint32_t kMaxLdsSpheres = 2048; // 64 KiB of LDS geometry; above this, read from global
+constexpr int kBlock = 256;                // 4 waves of 64 lanes
+constexpr uint32_t kMaxLdsSpheres = 2048;  // 64 KiB of LDS geometry; above this, read from global
+constexpr uint32_t kChunk = 2048;          // work items a wave claims per queue fetch
 
 // Geometry walked by every lane for every ray: 32 B, one LDS broadcast pair per sphere.
 struct alignas(32) GeoRec {
@@ -25,7 +26,10 @@ struct alignas(16) MatRec {
     uint32_t pad;
 };
 
-// Kernel arguments (by value).  Mirrors rt_camera + the row partition.
+// Arguments of the sample kernel (by value).  One launch renders the samples
+// [s_begin, s_begin + s_count) of the rows j = row0 + k*row_step, k < n_rows.
+// Work item t in [0, s_count * n_rows * W): sample s_begin + t / P of local pixel q = t % P
+// (P = n_rows * W); its color goes to samples[3*t .. 3*t+2].
 struct KernelParams {
     uint32_t width, height, spp, bounce_max;
     double scale;  // pixelSamplesScale
@@ -33,12 +37,24 @@ struct KernelParams {
     double defocus_angle, t_min, t_max;
     uint64_t seed_mix;  // sm_mix(seed), hoisted from sample_key
     uint32_t row0, row_step, n_rows, n_spheres;
-    uint32_t out_format;  // 0 linear f64, 1 rgb8
+    uint32_t s_begin, s_count;
+};
+
+// Arguments of the ordered reduction: pixel q's running sum += samples[s][q] for s = 0..s_count-1
+// (exactly the reference's sequential `pixelColor += rayColor(ray)`, camera.zig:133-136).
+struct ReduceParams {
+    uint32_t n_pixels, s_count;
+    uint32_t first, last;   // first chunk starts from 0; last chunk scales and writes the output
+    uint32_t out_format;    // 0 linear f64 (3 doubles per pixel), 1 rgb8
     uint32_t pad;
+    double scale;
 };
 
 }  // namespace rtk
 
-extern "C" hipError_t rtk_launch_render(const rtk::KernelParams* p, const rtk::GeoRec* geo,
-                                        const rtk::MatRec* mat, void* out, void* stats,
-                                        hipStream_t stream, const char** name);
+// Launch wrappers (rt_kernel.hip); all asynchronous on `stream`.
+extern "C" hipError_t rtk_launch_samples(const rtk::KernelParams* p, const rtk::GeoRec* geo,
+                                         const rtk::MatRec* mat, double* samples, void* queue,
+                                         void* stats, hipStream_t stream, const char** name);
+extern "C" hipError_t rtk_launch_reduce(const rtk::ReduceParams* p, const double* samples,
+                                        double* sums, void* out, hipStream_t stream);

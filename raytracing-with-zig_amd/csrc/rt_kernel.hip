@@ -1,23 +1,28 @@
-// rt_kernel.hip — the per-pixel x per-sample megakernel (gfx950 / CDNA4).
+// rt_kernel.hip — the per-pixel x per-sample hot path on gfx950 (CDNA4).
 //
 // Replaces the loop nest of Camera.render (reference src/camera.zig:123-145):
 //   for j, for i, for s: getRay (camera.zig:187-215) -> rayColor (camera.zig:148-183)
 //     -> HittableList.hit (hittable.zig:64-77) -> Sphere.hit (sphere.zig:26-54)
 //     -> Material.scatter (material.zig:145-151)
 //
-// Mapping (DESIGN.md "Kernel"):
-//   * one lane = one pixel; the lane sums its samples s = 0..spp-1 in order, exactly like
-//     camera.zig:133-138, so the f64 sum rounds identically;
-//   * the bounce loop and the sample loop are FLATTENED into one loop of ray segments: a lane whose
-//     path ends (miss / absorb / bounceMax) immediately starts its next sample, so a wave pays
-//     max-over-lanes of total rays, not sum-over-samples of max bounces;
-//   * sphere geometry {cx, cy, cz, r^2} is staged once per workgroup into LDS (32 B per sphere);
-//     every lane walks the list in order and all lanes of a wave read the same sphere (LDS
-//     broadcast, conflict-free); materials are read from global memory only for the hit sphere;
-//   * the closest-hit scan keeps the reference's exact acceptance rule (strict surrounds on the
-//     shrinking (t_min, closest) interval) and computes the hit record only for the winner — the
-//     same bits as recomputing it per accepted sphere;
-//   * output is written once per pixel (coalesced: consecutive lanes, consecutive pixels).
+// Two kernels (DESIGN.md "Kernels"):
+//
+// sample_kernel — persistent waves pull work items (one item = one sample of one pixel) from a
+//   global queue, 2048 items per wave per atomic.  A lane whose path ends (miss / absorb /
+//   bounceMax) stores the sample's color and immediately takes the next item, so every lane of
+//   every wave traces one ray segment per loop iteration until the queue drains: no lane idles
+//   behind a long glass path and no CU idles behind a slow block.
+//   Sphere geometry {cx, cy, cz, r^2} is staged once per workgroup into LDS (32 B per sphere);
+//   every lane walks the list in order and all lanes of a wave read the same sphere (LDS
+//   broadcast, conflict-free).  Materials are read from global memory for the hit sphere only.
+//   The closest-hit scan keeps the reference's acceptance rule (strict surrounds on the shrinking
+//   interval) and computes the hit record for the winner only — the same bits as the reference's
+//   per-accepted-sphere record.
+//
+// reduce_kernel — per pixel, adds the stored sample colors in sample order to a running f64 sum
+//   (camera.zig:135 `pixelColor += rayColor(ray)` — the same sequence of roundings as the
+//   reference's loop), then scales by pixelSamplesScale (camera.zig:137) and writes linear f64 or
+//   the fused Color.toRgb bytes (color.zig:63-80).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -53,7 +58,6 @@ __device__ __forceinline__ Ray get_ray(const KernelParams& p, uint32_t i, uint32
 
 // HittableList.hit over Sphere.hit with the exact arithmetic of sphere.zig:27-41.
 // Returns the winning sphere index (or -1); *t_hit = its root.
-template <bool kLds>
 __device__ __forceinline__ int world_hit(const GeoRec* __restrict__ geo, uint32_t n, const Ray& r,
                                          double t_min, double t_max, double* t_hit) {
     const double a = len_sq(r.dir);  // loop-invariant Vec.lenSquared(ray.dir)
@@ -85,11 +89,20 @@ __device__ __forceinline__ int world_hit(const GeoRec* __restrict__ geo, uint32_
     return best;
 }
 
-template <bool kLds, int kOut>
-__global__ __launch_bounds__(kBlock) void render_kernel(KernelParams p,
+__device__ __forceinline__ uint32_t lane_id() {
+    return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+}
+// number of set bits of `mask` below this lane
+__device__ __forceinline__ uint32_t rank_in(uint64_t mask) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+}
+
+template <bool kLds>
+__global__ __launch_bounds__(kBlock) void sample_kernel(KernelParams p,
                                                         const GeoRec* __restrict__ geo_g,
                                                         const MatRec* __restrict__ mat_g,
-                                                        void* __restrict__ out,
+                                                        double* __restrict__ samples,
+                                                        unsigned long long* __restrict__ queue,
                                                         unsigned long long* __restrict__ stats) {
     extern __shared__ GeoRec lds_geo[];
     const GeoRec* geo = geo_g;
@@ -100,34 +113,73 @@ __global__ __launch_bounds__(kBlock) void render_kernel(KernelParams p,
     }
 
     const uint32_t W = p.width;
-    const uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const bool valid = q < (uint64_t)p.n_rows * W;
-    uint64_t rays = 0;
-    uint64_t samples = 0;
+    const uint32_t P = p.n_rows * W;           // pixels per sample layer
+    const uint64_t total = (uint64_t)P * p.s_count;
+    const uint32_t lane = lane_id();
 
-    if (valid) {
-        const uint32_t row_local = (uint32_t)(q / W);
-        const uint32_t i = (uint32_t)(q - (uint64_t)row_local * W);
-        const uint32_t j = p.row0 + row_local * p.row_step;
-        const uint64_t pixel = (uint64_t)j * W + i;
+    // wave-uniform queue window [cur, end)
+    uint64_t cur = 0, end = 0;
+    bool drained = false;
 
-        v3 sum = mk(0, 0, 0);
-        uint32_t s = 0;
-        Rng g;
-        g.seed(sample_key(p.seed_mix, pixel, s));
-        Ray r = get_ray(p, i, j, g);
-        v3 att = mk(1, 1, 1);
-        uint32_t bounce = 0;
+    // per-lane path state
+    bool active = false;
+    uint64_t item = 0;
+    Rng g;
+    Ray r;
+    v3 att = mk(1, 1, 1);
+    uint32_t bounce = 0;
+    uint64_t rays = 0, nsamples = 0;
 
-        while (true) {
+    while (true) {
+        // ---- hand new items to lanes without a path (wave-uniform control flow) ----------------
+        uint64_t needy = __ballot(!active);
+        while (needy != 0 && !drained) {
+            if (cur >= end) {
+                unsigned long long base = 0;
+                if (lane == 0) base = atomicAdd(queue, (unsigned long long)kChunk);
+                base = __shfl(base, 0, 64);
+                if (base >= total) {
+                    drained = true;
+                    break;
+                }
+                cur = base;
+                end = base + kChunk < total ? base + kChunk : total;
+            }
+            const uint64_t avail = end - cur;
+            const uint32_t want = (uint32_t)__popcll(needy);
+            const uint32_t take = avail < want ? (uint32_t)avail : want;
+            if (!active) {
+                const uint32_t rk = rank_in(needy);
+                if (rk < take) {
+                    item = cur + rk;
+                    active = true;
+                    const uint32_t s_local = (uint32_t)(item / P);
+                    const uint32_t q = (uint32_t)(item - (uint64_t)s_local * P);
+                    const uint32_t row_local = q / W;
+                    const uint32_t i = q - row_local * W;
+                    const uint32_t j = p.row0 + row_local * p.row_step;
+                    const uint64_t pixel = (uint64_t)j * W + i;
+                    g.seed(sample_key(p.seed_mix, pixel, p.s_begin + s_local));
+                    r = get_ray(p, i, j, g);
+                    att = mk(1, 1, 1);
+                    bounce = 0;
+                }
+            }
+            cur += take;
+            needy = __ballot(!active);
+        }
+        if (__ballot(active) == 0) break;
+
+        // ---- trace one ray segment per active lane (rayColor's loop body, camera.zig:153-177) --
+        if (active) {
             bool done;
             v3 col = mk(0, 0, 0);
             if (bounce >= p.bounce_max) {
-                done = true;  // rayColor fall-through: too many bounces -> black (camera.zig:181)
+                done = true;  // too many bounces -> black (camera.zig:181)
             } else {
                 double t;
                 ++rays;
-                const int k = world_hit<kLds>(geo, p.n_spheres, r, p.t_min, p.t_max, &t);
+                const int k = world_hit(geo, p.n_spheres, r, p.t_min, p.t_max, &t);
                 if (k < 0) {
                     // sky gradient (camera.zig:171-177)
                     const double a = 0.5 * (unit(r.dir).y + 1.0);
@@ -180,79 +232,128 @@ __global__ __launch_bounds__(kBlock) void render_kernel(KernelParams p,
                 }
             }
             if (done) {
-                sum = sum + col;  // pixelColor += rayColor(ray) (camera.zig:135)
-                ++samples;
-                if (++s >= p.spp) break;
-                g.seed(sample_key(p.seed_mix, pixel, s));
-                r = get_ray(p, i, j, g);
-                att = mk(1, 1, 1);
-                bounce = 0;
+                double* dst = samples + 3 * item;
+                dst[0] = col.x;
+                dst[1] = col.y;
+                dst[2] = col.z;
+                ++nsamples;
+                active = false;
             }
-        }
-
-        const v3 avg = muls(sum, p.scale);  // camera.zig:137
-        const uint64_t o = (uint64_t)row_local * W + i;
-        if constexpr (kOut == 0) {
-            double* dst = (double*)out + 3 * o;
-            dst[0] = avg.x;
-            dst[1] = avg.y;
-            dst[2] = avg.z;
-        } else {
-            uint8_t* dst = (uint8_t*)out + 3 * o;
-            dst[0] = to_byte(avg.x);
-            dst[1] = to_byte(avg.y);
-            dst[2] = to_byte(avg.z);
         }
     }
 
     if (stats) {
-        // wave-level reduction, one atomic pair per wave
+        // wave-level reduction, one atomic pair per wave (all lanes converged here)
         for (int off = 32; off > 0; off >>= 1) {
             rays += __shfl_xor(rays, off, 64);
-            samples += __shfl_xor(samples, off, 64);
+            nsamples += __shfl_xor(nsamples, off, 64);
         }
-        if ((threadIdx.x & 63) == 0) {
+        if (lane == 0) {
             atomicAdd(&stats[0], (unsigned long long)rays);
-            atomicAdd(&stats[1], (unsigned long long)samples);
+            atomicAdd(&stats[1], (unsigned long long)nsamples);
         }
+    }
+}
+
+template <int kOut>
+__global__ __launch_bounds__(256) void reduce_kernel(ReduceParams p, const double* __restrict__ samples,
+                                                     double* __restrict__ sums, void* __restrict__ out) {
+    const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= p.n_pixels) return;
+    double x = 0.0, y = 0.0, z = 0.0;
+    if (!p.first) {
+        x = sums[3 * (uint64_t)q + 0];
+        y = sums[3 * (uint64_t)q + 1];
+        z = sums[3 * (uint64_t)q + 2];
+    }
+    const double* src = samples + 3 * (uint64_t)q;
+    const uint64_t stride = 3 * (uint64_t)p.n_pixels;
+    for (uint32_t s = 0; s < p.s_count; ++s) {
+        x = x + src[0];
+        y = y + src[1];
+        z = z + src[2];
+        src += stride;
+    }
+    if (!p.last) {
+        sums[3 * (uint64_t)q + 0] = x;
+        sums[3 * (uint64_t)q + 1] = y;
+        sums[3 * (uint64_t)q + 2] = z;
+        return;
+    }
+    // avgColor = pixelColor * pixelSamplesScale (camera.zig:137)
+    x = x * p.scale;
+    y = y * p.scale;
+    z = z * p.scale;
+    if constexpr (kOut == 0) {
+        double* dst = (double*)out + 3 * (uint64_t)q;
+        dst[0] = x;
+        dst[1] = y;
+        dst[2] = z;
+    } else {
+        uint8_t* dst = (uint8_t*)out + 3 * (uint64_t)q;
+        dst[0] = to_byte(x);
+        dst[1] = to_byte(y);
+        dst[2] = to_byte(z);
     }
 }
 
 }  // namespace rtk
 
 // ------------------------------------------------------------------------------------------------
-// launch wrapper (called from rt_runtime.cpp)
+// launch wrappers (called from rt_runtime.cpp)
 // ------------------------------------------------------------------------------------------------
-extern "C" hipError_t rtk_launch_render(const rtk::KernelParams* p, const rtk::GeoRec* geo,
-                                        const rtk::MatRec* mat, void* out, void* stats,
-                                        hipStream_t stream, const char** name) {
+namespace {
+
+template <bool kLds>
+uint32_t persistent_blocks(size_t shmem) {
+    // A persistent grid: as many blocks as can be resident (CUs x blocks per CU).  If the
+    // occupancy query over-reports, the surplus blocks start late and simply find less work.
+    int dev = 0, cus = 0, per_cu = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 1024;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, rtk::sample_kernel<kLds>, rtk::kBlock, shmem) != hipSuccess ||
+        per_cu <= 0)
+        per_cu = 4;
+    return (uint32_t)(cus * per_cu);
+}
+
+}  // namespace
+
+extern "C" hipError_t rtk_launch_samples(const rtk::KernelParams* p, const rtk::GeoRec* geo,
+                                         const rtk::MatRec* mat, double* samples, void* queue,
+                                         void* stats, hipStream_t stream, const char** name) {
     using namespace rtk;
-    const uint64_t total = (uint64_t)p->n_rows * p->width;
+    const uint64_t total = (uint64_t)p->n_rows * p->width * p->s_count;
     if (total == 0) return hipSuccess;
-    const uint32_t blocks = (uint32_t)((total + kBlock - 1) / kBlock);
     const bool lds = p->n_spheres <= kMaxLdsSpheres;
     const size_t shmem = lds ? (size_t)p->n_spheres * sizeof(GeoRec) : 0;
+    const uint64_t need = (total + kBlock - 1) / kBlock;
     auto* st = (unsigned long long*)stats;
+    auto* qu = (unsigned long long*)queue;
+    hipError_t e = hipMemsetAsync(queue, 0, sizeof(unsigned long long), stream);
+    if (e != hipSuccess) return e;
     if (lds) {
-        if (p->out_format == 0) {
-            if (name) *name = "render_kernel<lds,f64>";
-            hipLaunchKernelGGL((render_kernel<true, 0>), dim3(blocks), dim3(kBlock), shmem, stream,
-                               *p, geo, mat, out, st);
-        } else {
-            if (name) *name = "render_kernel<lds,rgb8>";
-            hipLaunchKernelGGL((render_kernel<true, 1>), dim3(blocks), dim3(kBlock), shmem, stream,
-                               *p, geo, mat, out, st);
-        }
+        const uint32_t blocks = (uint32_t)(need < persistent_blocks<true>(shmem) ? need : persistent_blocks<true>(shmem));
+        if (name) *name = "sample_kernel<lds>";
+        hipLaunchKernelGGL((sample_kernel<true>), dim3(blocks), dim3(kBlock), shmem, stream, *p, geo, mat,
+                           samples, qu, st);
     } else {
-        if (p->out_format == 0) {
-            if (name) *name = "render_kernel<global,f64>";
-            hipLaunchKernelGGL((render_kernel<false, 0>), dim3(blocks), dim3(kBlock), 0, stream,
-                               *p, geo, mat, out, st);
-        } else {
-            if (name) *name = "render_kernel<global,rgb8>";
-            hipLaunchKernelGGL((render_kernel<false, 1>), dim3(blocks), dim3(kBlock), 0, stream,
-                               *p, geo, mat, out, st);
-        }
+        const uint32_t blocks = (uint32_t)(need < persistent_blocks<false>(0) ? need : persistent_blocks<false>(0));
+        if (name) *name = "sample_kernel<global>";
+        hipLaunchKernelGGL((sample_kernel<false>), dim3(blocks), dim3(kBlock), 0, stream, *p, geo, mat,
+                           samples, qu, st);
     }
+    return hipGetLastError();
+}
+
+extern "C" hipError_t rtk_launch_reduce(const rtk::ReduceParams* p, const double* samples, double* sums,
+                                        void* out, hipStream_t stream) {
+    using namespace rtk;
+    if (p->n_pixels == 0) return hipSuccess;
+    const uint32_t blocks = (p->n_pixels + 255) / 256;
+    if (p->out_format == 0)
+        hipLaunchKernelGGL((reduce_kernel<0>), dim3(blocks), dim3(256), 0, stream, *p, samples, sums, out);
+    else
+        hipLaunchKernelGGL((reduce_kernel<1>), dim3(blocks), dim3(256), 0, stream, *p, samples, sums, out);
     return hipGetLastError();
 }

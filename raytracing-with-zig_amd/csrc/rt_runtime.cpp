@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cmath>
 #include <cstring>
 #include <string>
@@ -27,7 +28,14 @@ struct rt_context {
     rtk::MatRec* d_mat = nullptr;
     uint32_t n_spheres = 0;
     uint32_t capacity = 0;
-    const char* last_kernel = "render_kernel";
+    // workspace: per-sample colors [s][pixel][3] (HBM is 288 GB: a whole 1200x800x500 frame of
+    // samples is 11.5 GB), running per-pixel sums for multi-chunk renders, the work-queue counter
+    double* d_samples = nullptr;
+    size_t samples_bytes = 0;
+    double* d_sums = nullptr;
+    size_t sums_bytes = 0;
+    unsigned long long* d_queue = nullptr;
+    const char* last_kernel = "sample_kernel";
 };
 
 namespace {
@@ -76,6 +84,30 @@ int validate_spheres(const rt_sphere* s, size_t n) {
     return RT_OK;
 }
 
+// Workspace budget for per-sample colors: RTZIG_WORKSPACE_MB, default 16 GiB (MI355X has 288 GB
+// of HBM; a whole config-4 frame needs 11.5 GB), never more than 60% of the free memory.
+uint64_t workspace_budget() {
+    uint64_t budget = 16ULL << 30;
+    if (const char* e = std::getenv("RTZIG_WORKSPACE_MB")) budget = std::strtoull(e, nullptr, 10) << 20;
+    size_t free_b = 0, total_b = 0;
+    if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b > 0) {
+        const uint64_t cap = (uint64_t)(0.6 * (double)free_b);
+        if (budget > cap) budget = cap;
+    }
+    return budget;
+}
+
+int ensure_buffer(void** ptr, size_t* bytes, size_t need) {
+    if (*ptr && *bytes >= need) return RT_OK;
+    (void)hipFree(*ptr);
+    *ptr = nullptr;
+    *bytes = 0;
+    hipError_t e = hipMalloc(ptr, need ? need : 1);
+    if (e != hipSuccess) return hip_fail(e, "hipMalloc(workspace)");
+    *bytes = need;
+    return RT_OK;
+}
+
 rtk::KernelParams make_params(const rt_camera* c, uint32_t fmt, uint32_t row0, uint32_t row_step,
                               uint32_t n_rows, uint32_t n_spheres) {
     rtk::KernelParams p;
@@ -101,7 +133,7 @@ rtk::KernelParams make_params(const rt_camera* c, uint32_t fmt, uint32_t row0, u
     p.row_step = row_step;
     p.n_rows = n_rows;
     p.n_spheres = n_spheres;
-    p.out_format = fmt;
+    (void)fmt;
     return p;
 }
 
@@ -142,6 +174,9 @@ int rt_context_destroy(rt_context* ctx) {
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     (void)hipFree(ctx->d_geo);
     (void)hipFree(ctx->d_mat);
+    (void)hipFree(ctx->d_samples);
+    (void)hipFree(ctx->d_sums);
+    (void)hipFree(ctx->d_queue);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
     return RT_OK;
@@ -200,9 +235,39 @@ int rt_render_rows_async(rt_context* ctx, const rt_camera* cam, uint32_t output_
         return RT_ERR_INVALID;
     }
     HIP_CHECK(hipSetDevice(ctx->device));
-    const rtk::KernelParams p = make_params(cam, output_format, row0, row_step, n_rows, ctx->n_spheres);
     hipStream_t s = (hipStream_t)stream;  // NULL = the HIP null stream, like torch's default stream
-    HIP_CHECK(rtk_launch_render(&p, ctx->d_geo, ctx->d_mat, d_out, d_stats, s, &ctx->last_kernel));
+
+    // Chunk the samples so that [s_count][P][3] doubles fit the workspace budget.
+    const uint64_t P = (uint64_t)n_rows * cam->image_width;
+    const uint64_t layer = P * 3 * sizeof(double);
+    uint64_t s_chunk = workspace_budget() / layer;
+    if (s_chunk < 1) s_chunk = 1;
+    if (s_chunk > cam->samples_per_pixel) s_chunk = cam->samples_per_pixel;
+    const uint32_t n_chunks = (uint32_t)((cam->samples_per_pixel + s_chunk - 1) / s_chunk);
+    rc = ensure_buffer((void**)&ctx->d_samples, &ctx->samples_bytes, s_chunk * layer);
+    if (!rc && n_chunks > 1) rc = ensure_buffer((void**)&ctx->d_sums, &ctx->sums_bytes, layer);
+    if (!rc && !ctx->d_queue) {
+        size_t qb = 0;
+        rc = ensure_buffer((void**)&ctx->d_queue, &qb, sizeof(unsigned long long));
+    }
+    if (rc) return rc;
+
+    rtk::KernelParams p = make_params(cam, output_format, row0, row_step, n_rows, ctx->n_spheres);
+    for (uint32_t c = 0; c < n_chunks; c++) {
+        p.s_begin = (uint32_t)(c * s_chunk);
+        p.s_count = (uint32_t)std::min<uint64_t>(s_chunk, cam->samples_per_pixel - p.s_begin);
+        HIP_CHECK(rtk_launch_samples(&p, ctx->d_geo, ctx->d_mat, ctx->d_samples, ctx->d_queue, d_stats, s,
+                                     &ctx->last_kernel));
+        rtk::ReduceParams rp;
+        std::memset(&rp, 0, sizeof rp);
+        rp.n_pixels = (uint32_t)P;
+        rp.s_count = p.s_count;
+        rp.first = c == 0;
+        rp.last = c + 1 == n_chunks;
+        rp.out_format = output_format;
+        rp.scale = cam->pixel_samples_scale;
+        HIP_CHECK(rtk_launch_reduce(&rp, ctx->d_samples, ctx->d_sums, d_out, s));
+    }
     return RT_OK;
 }
 
