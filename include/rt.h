@@ -118,6 +118,11 @@ int rt_render_rows_async(rt_context* ctx, const rt_camera* cam, uint32_t output_
                          void* d_out, void* d_stats, void* stream);
 /* Name of the kernel variant the context launches (for profiling / logs). */
 const char* rt_kernel_name(rt_context* ctx);
+/* Optional per-kernel timing with HIP events recorded on the launch stream around every sample and
+ * reduce kernel of a render call.  rt_context_kernel_times waits for the last event and returns the
+ * summed durations (ms) of the most recent rt_render_rows_async call. */
+int rt_context_enable_timing(rt_context* ctx, int enable);
+int rt_context_kernel_times(rt_context* ctx, double* sample_ms, double* reduce_ms);
 
 /* ---- host mirror of the reference's Scene / CameraBuilder / Color / PPM ---------------------- */
 /* Scene.generateWorld (Scene.zig:48-134) driven by DefaultPrng.init(seed) (Scene.zig:30).

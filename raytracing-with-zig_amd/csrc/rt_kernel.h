@@ -9,8 +9,12 @@ namespace rtk {
 constexpr int kBlock = 256;                // 4 waves of 64 lanes
 constexpr uint32_t kMaxLdsSpheres = 2048;  // 64 KiB of LDS geometry; above this, read from global
 constexpr uint32_t kChunk = 2048;          // work items a wave claims per queue fetch
+constexpr uint32_t kPad = 4;               // sphere list padded to a multiple of this (sentinels)
+constexpr int kDefaultUnroll = 2;          // spheres per step of the closest-hit walk
 
 // Geometry walked by every lane for every ray: 32 B, one LDS broadcast pair per sphere.
+// Padding entries are sentinels {0, 0, 0, -inf}: c = |oc|^2 + inf = +inf, so disc = -inf (or NaN
+// for a zero direction) and the sentinel never passes `disc >= 0`.
 struct alignas(32) GeoRec {
     double cx, cy, cz;  // Sphere.center
     double r2;          // radius * radius (hoisted from sphere.zig:30; same bits)
@@ -37,7 +41,9 @@ struct KernelParams {
     double defocus_angle, t_min, t_max;
     uint64_t seed_mix;  // sm_mix(seed), hoisted from sample_key
     uint32_t row0, row_step, n_rows, n_spheres;
+    uint32_t n_pad;  // n_spheres rounded up to kPad (sentinel-padded)
     uint32_t s_begin, s_count;
+    uint32_t pad_;
 };
 
 // Arguments of the ordered reduction: pixel q's running sum += samples[s][q] for s = 0..s_count-1

@@ -26,6 +26,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <cstdlib>
+
 #include "rt_device.h"
 #include "rt_kernel.h"
 
@@ -57,31 +59,42 @@ __device__ __forceinline__ Ray get_ray(const KernelParams& p, uint32_t i, uint32
 }
 
 // HittableList.hit over Sphere.hit with the exact arithmetic of sphere.zig:27-41.
-// Returns the winning sphere index (or -1); *t_hit = its root.
-__device__ __forceinline__ int world_hit(const GeoRec* __restrict__ geo, uint32_t n, const Ray& r,
+// Walks `n_pad` entries (the list padded to a multiple of kPad with never-hit sentinels, see
+// GeoRec) U spheres at a time: the U discriminants are independent, so their f64 chains and LDS
+// reads interleave; the hit tests then run in list order, so `closest` evolves exactly as in the
+// reference.  Returns the winning sphere index (or -1); *t_hit = its root.
+template <int U>
+__device__ __forceinline__ int world_hit(const GeoRec* __restrict__ geo, uint32_t n_pad, const Ray& r,
                                          double t_min, double t_max, double* t_hit) {
     const double a = len_sq(r.dir);  // loop-invariant Vec.lenSquared(ray.dir)
     double closest = t_max;
     int best = -1;
-    for (uint32_t k = 0; k < n; ++k) {
-        const GeoRec s = geo[k];
-        const double ocx = s.cx - r.orig.x;
-        const double ocy = s.cy - r.orig.y;
-        const double ocz = s.cz - r.orig.z;
-        const double h = (r.dir.x * ocx + r.dir.y * ocy) + r.dir.z * ocz;
-        const double c = ((ocx * ocx + ocy * ocy) + ocz * ocz) - s.r2;
-        const double disc = h * h - a * c;
-        if (disc >= 0) {  // !(disc < 0); a NaN disc rejects either way
-            const double sq = __builtin_sqrt(disc);
-            double root = (h - sq) / a;
-            bool ok = t_min < root && root < closest;
-            if (!ok) {
-                root = (h + sq) / a;
-                ok = t_min < root && root < closest;
-            }
-            if (ok) {
-                closest = root;
-                best = (int)k;
+    for (uint32_t k = 0; k < n_pad; k += U) {
+        double h[U], disc[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const GeoRec s = geo[k + u];
+            const double ocx = s.cx - r.orig.x;
+            const double ocy = s.cy - r.orig.y;
+            const double ocz = s.cz - r.orig.z;
+            h[u] = (r.dir.x * ocx + r.dir.y * ocy) + r.dir.z * ocz;
+            const double c = ((ocx * ocx + ocy * ocy) + ocz * ocz) - s.r2;
+            disc[u] = h[u] * h[u] - a * c;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (disc[u] >= 0) {  // !(disc < 0); a NaN disc rejects either way
+                const double sq = __builtin_sqrt(disc[u]);
+                double root = (h[u] - sq) / a;
+                bool ok = t_min < root && root < closest;
+                if (!ok) {
+                    root = (h[u] + sq) / a;
+                    ok = t_min < root && root < closest;
+                }
+                if (ok) {
+                    closest = root;
+                    best = (int)(k + u);
+                }
             }
         }
     }
@@ -97,7 +110,7 @@ __device__ __forceinline__ uint32_t rank_in(uint64_t mask) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
 }
 
-template <bool kLds>
+template <bool kLds, int U>
 __global__ __launch_bounds__(kBlock) void sample_kernel(KernelParams p,
                                                         const GeoRec* __restrict__ geo_g,
                                                         const MatRec* __restrict__ mat_g,
@@ -107,7 +120,7 @@ __global__ __launch_bounds__(kBlock) void sample_kernel(KernelParams p,
     extern __shared__ GeoRec lds_geo[];
     const GeoRec* geo = geo_g;
     if constexpr (kLds) {
-        for (uint32_t k = threadIdx.x; k < p.n_spheres; k += blockDim.x) lds_geo[k] = geo_g[k];
+        for (uint32_t k = threadIdx.x; k < p.n_pad; k += blockDim.x) lds_geo[k] = geo_g[k];
         __syncthreads();
         geo = lds_geo;
     }
@@ -179,7 +192,7 @@ __global__ __launch_bounds__(kBlock) void sample_kernel(KernelParams p,
             } else {
                 double t;
                 ++rays;
-                const int k = world_hit(geo, p.n_spheres, r, p.t_min, p.t_max, &t);
+                const int k = world_hit<U>(geo, p.n_pad, r, p.t_min, p.t_max, &t);
                 if (k < 0) {
                     // sky gradient (camera.zig:171-177)
                     const double a = 0.5 * (unit(r.dir).y + 1.0);
@@ -304,17 +317,34 @@ __global__ __launch_bounds__(256) void reduce_kernel(ReduceParams p, const doubl
 // ------------------------------------------------------------------------------------------------
 namespace {
 
-template <bool kLds>
+template <bool kLds, int U>
 uint32_t persistent_blocks(size_t shmem) {
     // A persistent grid: as many blocks as can be resident (CUs x blocks per CU).  If the
     // occupancy query over-reports, the surplus blocks start late and simply find less work.
     int dev = 0, cus = 0, per_cu = 0;
     if (hipGetDevice(&dev) != hipSuccess) return 1024;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, rtk::sample_kernel<kLds>, rtk::kBlock, shmem) != hipSuccess ||
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, rtk::sample_kernel<kLds, U>, rtk::kBlock, shmem) !=
+            hipSuccess ||
         per_cu <= 0)
         per_cu = 4;
     return (uint32_t)(cus * per_cu);
+}
+
+template <bool kLds, int U>
+void launch_samples(const rtk::KernelParams* p, const rtk::GeoRec* geo, const rtk::MatRec* mat, double* samples,
+                    unsigned long long* qu, unsigned long long* st, hipStream_t stream, size_t shmem, uint64_t need) {
+    const uint32_t cap = persistent_blocks<kLds, U>(shmem);
+    const uint32_t blocks = (uint32_t)(need < cap ? need : cap);
+    hipLaunchKernelGGL((rtk::sample_kernel<kLds, U>), dim3(blocks), dim3(rtk::kBlock), shmem, stream, *p, geo, mat,
+                       samples, qu, st);
+}
+
+// Unroll factor of the sphere walk: RTZIG_UNROLL=1|2|4 (default kDefaultUnroll).
+int unroll_choice() {
+    const char* e = std::getenv("RTZIG_UNROLL");
+    const int u = e ? std::atoi(e) : rtk::kDefaultUnroll;
+    return (u == 1 || u == 2 || u == 4) ? u : rtk::kDefaultUnroll;
 }
 
 }  // namespace
@@ -325,23 +355,26 @@ extern "C" hipError_t rtk_launch_samples(const rtk::KernelParams* p, const rtk::
     using namespace rtk;
     const uint64_t total = (uint64_t)p->n_rows * p->width * p->s_count;
     if (total == 0) return hipSuccess;
-    const bool lds = p->n_spheres <= kMaxLdsSpheres;
-    const size_t shmem = lds ? (size_t)p->n_spheres * sizeof(GeoRec) : 0;
+    const bool lds = p->n_pad <= kMaxLdsSpheres;
+    const size_t shmem = lds ? (size_t)p->n_pad * sizeof(GeoRec) : 0;
     const uint64_t need = (total + kBlock - 1) / kBlock;
     auto* st = (unsigned long long*)stats;
     auto* qu = (unsigned long long*)queue;
     hipError_t e = hipMemsetAsync(queue, 0, sizeof(unsigned long long), stream);
     if (e != hipSuccess) return e;
+    static const char* names[2][5] = {
+        {"", "sample_kernel<global,u1>", "sample_kernel<global,u2>", "", "sample_kernel<global,u4>"},
+        {"", "sample_kernel<lds,u1>", "sample_kernel<lds,u2>", "", "sample_kernel<lds,u4>"}};
+    const int u = unroll_choice();
+    if (name) *name = names[lds ? 1 : 0][u];
     if (lds) {
-        const uint32_t blocks = (uint32_t)(need < persistent_blocks<true>(shmem) ? need : persistent_blocks<true>(shmem));
-        if (name) *name = "sample_kernel<lds>";
-        hipLaunchKernelGGL((sample_kernel<true>), dim3(blocks), dim3(kBlock), shmem, stream, *p, geo, mat,
-                           samples, qu, st);
+        if (u == 1) launch_samples<true, 1>(p, geo, mat, samples, qu, st, stream, shmem, need);
+        else if (u == 2) launch_samples<true, 2>(p, geo, mat, samples, qu, st, stream, shmem, need);
+        else launch_samples<true, 4>(p, geo, mat, samples, qu, st, stream, shmem, need);
     } else {
-        const uint32_t blocks = (uint32_t)(need < persistent_blocks<false>(0) ? need : persistent_blocks<false>(0));
-        if (name) *name = "sample_kernel<global>";
-        hipLaunchKernelGGL((sample_kernel<false>), dim3(blocks), dim3(kBlock), 0, stream, *p, geo, mat,
-                           samples, qu, st);
+        if (u == 1) launch_samples<false, 1>(p, geo, mat, samples, qu, st, stream, 0, need);
+        else if (u == 2) launch_samples<false, 2>(p, geo, mat, samples, qu, st, stream, 0, need);
+        else launch_samples<false, 4>(p, geo, mat, samples, qu, st, stream, 0, need);
     }
     return hipGetLastError();
 }

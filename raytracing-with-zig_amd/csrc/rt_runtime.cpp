@@ -12,6 +12,7 @@
 #include <cstdlib>
 #include <cmath>
 #include <cstring>
+#include <limits>
 #include <string>
 #include <vector>
 
@@ -36,6 +37,10 @@ struct rt_context {
     size_t sums_bytes = 0;
     unsigned long long* d_queue = nullptr;
     const char* last_kernel = "sample_kernel";
+    // optional per-kernel timing: event pairs around every sample / reduce launch of the last call
+    bool timing = false;
+    std::vector<hipEvent_t> events;  // pool; [4c..4c+3] = sample start/stop, reduce start/stop
+    uint32_t timed_chunks = 0;
 };
 
 namespace {
@@ -133,6 +138,7 @@ rtk::KernelParams make_params(const rt_camera* c, uint32_t fmt, uint32_t row0, u
     p.row_step = row_step;
     p.n_rows = n_rows;
     p.n_spheres = n_spheres;
+    p.n_pad = (n_spheres + rtk::kPad - 1) / rtk::kPad * rtk::kPad;
     (void)fmt;
     return p;
 }
@@ -177,6 +183,7 @@ int rt_context_destroy(rt_context* ctx) {
     (void)hipFree(ctx->d_samples);
     (void)hipFree(ctx->d_sums);
     (void)hipFree(ctx->d_queue);
+    for (hipEvent_t e : ctx->events) (void)hipEventDestroy(e);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
     return RT_OK;
@@ -187,8 +194,13 @@ int rt_context_set_scene(rt_context* ctx, const rt_sphere* spheres, size_t n) {
     int rc = validate_spheres(spheres, n);
     if (rc) return rc;
     HIP_CHECK(hipSetDevice(ctx->device));
-    std::vector<rtk::GeoRec> geo(n);
+    const size_t n_pad = (n + rtk::kPad - 1) / rtk::kPad * rtk::kPad;
+    std::vector<rtk::GeoRec> geo(n_pad);
     std::vector<rtk::MatRec> mat(n);
+    for (size_t k = n; k < n_pad; k++) {  // never-hit sentinels (rt_kernel.h)
+        geo[k].cx = geo[k].cy = geo[k].cz = 0.0;
+        geo[k].r2 = -std::numeric_limits<double>::infinity();
+    }
     for (size_t k = 0; k < n; k++) {
         const double r = spheres[k].radius > 0 ? spheres[k].radius : 0.0;  // sphere.zig:21
         geo[k].cx = spheres[k].center[0];
@@ -202,17 +214,17 @@ int rt_context_set_scene(rt_context* ctx, const rt_sphere* spheres, size_t n) {
         mat[k].inv_r = 1.0 / r;
         mat[k].kind = spheres[k].material;
     }
-    if (n > ctx->capacity) {
+    if (n_pad > ctx->capacity) {
         (void)hipFree(ctx->d_geo);
         (void)hipFree(ctx->d_mat);
         ctx->d_geo = nullptr;
         ctx->d_mat = nullptr;
         ctx->capacity = 0;
-        HIP_CHECK(hipMalloc(&ctx->d_geo, n * sizeof(rtk::GeoRec)));
-        HIP_CHECK(hipMalloc(&ctx->d_mat, n * sizeof(rtk::MatRec)));
-        ctx->capacity = (uint32_t)n;
+        HIP_CHECK(hipMalloc(&ctx->d_geo, n_pad * sizeof(rtk::GeoRec)));
+        HIP_CHECK(hipMalloc(&ctx->d_mat, n_pad * sizeof(rtk::MatRec)));
+        ctx->capacity = (uint32_t)n_pad;
     }
-    HIP_CHECK(hipMemcpyAsync(ctx->d_geo, geo.data(), n * sizeof(rtk::GeoRec), hipMemcpyHostToDevice, ctx->stream));
+    HIP_CHECK(hipMemcpyAsync(ctx->d_geo, geo.data(), n_pad * sizeof(rtk::GeoRec), hipMemcpyHostToDevice, ctx->stream));
     HIP_CHECK(hipMemcpyAsync(ctx->d_mat, mat.data(), n * sizeof(rtk::MatRec), hipMemcpyHostToDevice, ctx->stream));
     HIP_CHECK(hipStreamSynchronize(ctx->stream));
     ctx->n_spheres = (uint32_t)n;
@@ -252,12 +264,22 @@ int rt_render_rows_async(rt_context* ctx, const rt_camera* cam, uint32_t output_
     }
     if (rc) return rc;
 
+    if (ctx->timing) {
+        while (ctx->events.size() < 4 * (size_t)n_chunks) {
+            hipEvent_t e;
+            HIP_CHECK(hipEventCreate(&e));
+            ctx->events.push_back(e);
+        }
+        ctx->timed_chunks = n_chunks;
+    }
     rtk::KernelParams p = make_params(cam, output_format, row0, row_step, n_rows, ctx->n_spheres);
     for (uint32_t c = 0; c < n_chunks; c++) {
         p.s_begin = (uint32_t)(c * s_chunk);
         p.s_count = (uint32_t)std::min<uint64_t>(s_chunk, cam->samples_per_pixel - p.s_begin);
+        if (ctx->timing) HIP_CHECK(hipEventRecord(ctx->events[4 * c + 0], s));
         HIP_CHECK(rtk_launch_samples(&p, ctx->d_geo, ctx->d_mat, ctx->d_samples, ctx->d_queue, d_stats, s,
                                      &ctx->last_kernel));
+        if (ctx->timing) HIP_CHECK(hipEventRecord(ctx->events[4 * c + 1], s));
         rtk::ReduceParams rp;
         std::memset(&rp, 0, sizeof rp);
         rp.n_pixels = (uint32_t)P;
@@ -266,8 +288,35 @@ int rt_render_rows_async(rt_context* ctx, const rt_camera* cam, uint32_t output_
         rp.last = c + 1 == n_chunks;
         rp.out_format = output_format;
         rp.scale = cam->pixel_samples_scale;
+        if (ctx->timing) HIP_CHECK(hipEventRecord(ctx->events[4 * c + 2], s));
         HIP_CHECK(rtk_launch_reduce(&rp, ctx->d_samples, ctx->d_sums, d_out, s));
+        if (ctx->timing) HIP_CHECK(hipEventRecord(ctx->events[4 * c + 3], s));
     }
+    return RT_OK;
+}
+
+int rt_context_enable_timing(rt_context* ctx, int enable) {
+    if (!ctx) { rt_set_last_error("null context"); return RT_ERR_INVALID; }
+    ctx->timing = enable != 0;
+    ctx->timed_chunks = 0;
+    return RT_OK;
+}
+
+int rt_context_kernel_times(rt_context* ctx, double* sample_ms, double* reduce_ms) {
+    if (!ctx) { rt_set_last_error("null context"); return RT_ERR_INVALID; }
+    if (!ctx->timing || ctx->timed_chunks == 0) { rt_set_last_error("timing not enabled or nothing rendered"); return RT_ERR_INVALID; }
+    HIP_CHECK(hipSetDevice(ctx->device));
+    double sm = 0, rm = 0;
+    for (uint32_t c = 0; c < ctx->timed_chunks; c++) {
+        float a = 0, b = 0;
+        HIP_CHECK(hipEventSynchronize(ctx->events[4 * c + 3]));
+        HIP_CHECK(hipEventElapsedTime(&a, ctx->events[4 * c + 0], ctx->events[4 * c + 1]));
+        HIP_CHECK(hipEventElapsedTime(&b, ctx->events[4 * c + 2], ctx->events[4 * c + 3]));
+        sm += a;
+        rm += b;
+    }
+    if (sample_ms) *sample_ms = sm;
+    if (reduce_ms) *reduce_ms = rm;
     return RT_OK;
 }
 

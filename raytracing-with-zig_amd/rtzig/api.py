@@ -200,6 +200,15 @@ class DeviceRenderer:
     def kernel_name(self):
         return self.lib.rt_kernel_name(self.ctx).decode()
 
+    def enable_timing(self, enable=True):
+        check("rt_context_enable_timing", self.lib.rt_context_enable_timing(self.ctx, int(enable)))
+
+    def kernel_times(self):
+        """(sample_kernel_ms, reduce_kernel_ms) of the last render call (HIP events)."""
+        a, b = C.c_double(), C.c_double()
+        check("rt_context_kernel_times", self.lib.rt_context_kernel_times(self.ctx, C.byref(a), C.byref(b)))
+        return a.value, b.value
+
     def close(self):
         if self.ctx:
             self.lib.rt_context_destroy(self.ctx)

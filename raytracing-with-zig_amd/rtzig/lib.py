@@ -19,6 +19,8 @@ EXPORTED = [
     "rt_context_set_scene",
     "rt_render_rows_async",
     "rt_kernel_name",
+    "rt_context_enable_timing",
+    "rt_context_kernel_times",
     "rt_scene_final",
     "rt_scene_chapter13",
     "rt_camera_build",
@@ -52,6 +54,8 @@ def _declare(lib):
         "rt_render_rows_async": (C.c_int, [vp, P(RtCamera), C.c_uint32, C.c_uint32, C.c_uint32,
                                            C.c_uint32, vp, vp, vp]),
         "rt_kernel_name": (C.c_char_p, [vp]),
+        "rt_context_enable_timing": (C.c_int, [vp, C.c_int]),
+        "rt_context_kernel_times": (C.c_int, [vp, P(C.c_double), P(C.c_double)]),
         "rt_scene_final": (C.c_int, [C.c_uint64, P(RtSphere), C.c_size_t, P(C.c_size_t),
                                      P(C.c_uint64)]),
         "rt_scene_chapter13": (C.c_int, [P(RtSphere), C.c_size_t, P(C.c_size_t)]),

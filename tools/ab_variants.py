@@ -1,0 +1,57 @@
+#!/usr/bin/env python3
+"""A/B the sample-kernel variants IN ONE PROCESS, interleaved rounds (cdna guide rule 24).
+
+    RTZIG_VARIANTS="1 2 4" python tools/ab_variants.py --spp 100 --rounds 5
+Each variant is selected through RTZIG_UNROLL (read at every launch).  Prints one JSON line with
+per-variant median/min sample-kernel ms (HIP events) and Msamples/s.
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "raytracing-with-zig_amd"))
+import torch  # noqa: E402
+
+import rtzig  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--width", type=int, default=1200)
+ap.add_argument("--aspect", type=float, default=1.5)
+ap.add_argument("--spp", type=int, default=100)
+ap.add_argument("--rounds", type=int, default=5)
+ap.add_argument("--env", default="RTZIG_UNROLL")
+ap.add_argument("--variants", default=os.environ.get("RTZIG_VARIANTS", "1 2 4"))
+args = ap.parse_args()
+
+cam = rtzig.final_scene_camera(width=args.width, aspect_ratio=args.aspect, spp=args.spp)
+H, W = cam.height, cam.width
+r = rtzig.DeviceRenderer(0)
+r.set_scene(cam.scene.world)
+r.enable_timing(True)
+out = torch.empty((H, W, 3), dtype=torch.float64, device="cuda:0")
+variants = args.variants.split()
+times = {v: [] for v in variants}
+names = {}
+ref = None
+for rnd in range(args.rounds + 1):
+    for v in variants:
+        os.environ[args.env] = v
+        r.render_rows_async(cam.cam, out.data_ptr())
+        torch.cuda.synchronize()
+        sm, _ = r.kernel_times()
+        names[v] = r.kernel_name()
+        img = out.cpu()
+        if ref is None:
+            ref = img
+        assert torch.equal(img, ref), f"variant {v} output differs"
+        if rnd > 0:  # round 0 = warmup
+            times[v].append(sm)
+res = {}
+for v in variants:
+    med = statistics.median(times[v])
+    res[v] = {"kernel": names[v], "median_ms": round(med, 3), "min_ms": round(min(times[v]), 3),
+              "Msamples_s": round(W * H * args.spp / med / 1e3, 1)}
+print(json.dumps({"config": f"{W}x{H} {args.spp}spp", "env": args.env, "results": res}))
