@@ -27,6 +27,7 @@
 #include <stdint.h>
 
 #include <cstdlib>
+#include <cstring>
 
 #include "rt_device.h"
 #include "rt_kernel.h"
@@ -110,8 +111,8 @@ __device__ __forceinline__ uint32_t rank_in(uint64_t mask) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
 }
 
-template <bool kLds, int U>
-__global__ __launch_bounds__(kBlock) void sample_kernel(KernelParams p,
+template <bool kLds, int U, int kWaves>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kWaves))) void sample_kernel(KernelParams p,
                                                         const GeoRec* __restrict__ geo_g,
                                                         const MatRec* __restrict__ mat_g,
                                                         double* __restrict__ samples,
@@ -317,34 +318,49 @@ __global__ __launch_bounds__(256) void reduce_kernel(ReduceParams p, const doubl
 // ------------------------------------------------------------------------------------------------
 namespace {
 
-template <bool kLds, int U>
-uint32_t persistent_blocks(size_t shmem) {
-    // A persistent grid: as many blocks as can be resident (CUs x blocks per CU).  If the
-    // occupancy query over-reports, the surplus blocks start late and simply find less work.
+// A persistent grid: as many blocks as can be resident (CUs x blocks per CU).  If the occupancy
+// query over-reports, the surplus blocks start late and simply find less work.
+template <typename K>
+uint32_t persistent_blocks(K kernel, size_t shmem) {
     int dev = 0, cus = 0, per_cu = 0;
     if (hipGetDevice(&dev) != hipSuccess) return 1024;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, rtk::sample_kernel<kLds, U>, rtk::kBlock, shmem) !=
-            hipSuccess ||
-        per_cu <= 0)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, rtk::kBlock, shmem) != hipSuccess || per_cu <= 0)
         per_cu = 4;
     return (uint32_t)(cus * per_cu);
 }
 
-template <bool kLds, int U>
+template <bool kLds, int U, int kWaves>
 void launch_samples(const rtk::KernelParams* p, const rtk::GeoRec* geo, const rtk::MatRec* mat, double* samples,
                     unsigned long long* qu, unsigned long long* st, hipStream_t stream, size_t shmem, uint64_t need) {
-    const uint32_t cap = persistent_blocks<kLds, U>(shmem);
+    auto kernel = rtk::sample_kernel<kLds, U, kWaves>;
+    const uint32_t cap = persistent_blocks(kernel, shmem);
     const uint32_t blocks = (uint32_t)(need < cap ? need : cap);
-    hipLaunchKernelGGL((rtk::sample_kernel<kLds, U>), dim3(blocks), dim3(rtk::kBlock), shmem, stream, *p, geo, mat,
-                       samples, qu, st);
+    hipLaunchKernelGGL(kernel, dim3(blocks), dim3(rtk::kBlock), shmem, stream, *p, geo, mat, samples, qu, st);
 }
 
-// Unroll factor of the sphere walk: RTZIG_UNROLL=1|2|4 (default kDefaultUnroll).
-int unroll_choice() {
-    const char* e = std::getenv("RTZIG_UNROLL");
-    const int u = e ? std::atoi(e) : rtk::kDefaultUnroll;
-    return (u == 1 || u == 2 || u == 4) ? u : rtk::kDefaultUnroll;
+// Kernel variant: RTZIG_KERNEL=<geom>_u<U>[_w<waves>], geom in {lds, smem}; default kDefaultVariant.
+//   lds  — sphere geometry staged in LDS, read by ds_read_b128 broadcasts
+//   smem — geometry read from global memory by scalar loads (s_load_dwordx16), SGPR operands
+struct Variant {
+    const char* name;
+    bool lds;
+    int unroll;
+    int waves;
+};
+constexpr Variant kVariants[] = {
+    {"lds_u1", true, 1, 1},  {"lds_u2", true, 2, 1},  {"lds_u4", true, 4, 1},  {"lds_u4_w5", true, 4, 5},
+    {"smem_u1", false, 1, 1}, {"smem_u2", false, 2, 1}, {"smem_u4", false, 4, 1}, {"smem_u4_w5", false, 4, 5},
+};
+
+const Variant& variant_choice(bool fits_lds) {
+    const char* e = std::getenv("RTZIG_KERNEL");
+    const char* want = e ? e : rtk::kDefaultVariant;
+    for (const Variant& v : kVariants)
+        if (std::strcmp(v.name, want) == 0 && (fits_lds || !v.lds)) return v;
+    for (const Variant& v : kVariants)
+        if (std::strcmp(v.name, rtk::kDefaultVariant) == 0 && (fits_lds || !v.lds)) return v;
+    return kVariants[6];  // smem_u4: works for any sphere count
 }
 
 }  // namespace
@@ -355,28 +371,23 @@ extern "C" hipError_t rtk_launch_samples(const rtk::KernelParams* p, const rtk::
     using namespace rtk;
     const uint64_t total = (uint64_t)p->n_rows * p->width * p->s_count;
     if (total == 0) return hipSuccess;
-    const bool lds = p->n_pad <= kMaxLdsSpheres;
-    const size_t shmem = lds ? (size_t)p->n_pad * sizeof(GeoRec) : 0;
+    const Variant& v = variant_choice(p->n_pad <= kMaxLdsSpheres);
+    const size_t shmem = v.lds ? (size_t)p->n_pad * sizeof(GeoRec) : 0;
     const uint64_t need = (total + kBlock - 1) / kBlock;
     auto* st = (unsigned long long*)stats;
     auto* qu = (unsigned long long*)queue;
     hipError_t e = hipMemsetAsync(queue, 0, sizeof(unsigned long long), stream);
     if (e != hipSuccess) return e;
-    static const char* names[2][5] = {
-        {"", "sample_kernel<global,u1>", "sample_kernel<global,u2>", "", "sample_kernel<global,u4>"},
-        {"", "sample_kernel<lds,u1>", "sample_kernel<lds,u2>", "", "sample_kernel<lds,u4>"}};
-    const int u = unroll_choice();
-    if (name) *name = names[lds ? 1 : 0][u];
-    if (lds) {
-        if (u == 1) launch_samples<true, 1>(p, geo, mat, samples, qu, st, stream, shmem, need);
-        else if (u == 2) launch_samples<true, 2>(p, geo, mat, samples, qu, st, stream, shmem, need);
-        else launch_samples<true, 4>(p, geo, mat, samples, qu, st, stream, shmem, need);
-    } else {
-        if (u == 1) launch_samples<false, 1>(p, geo, mat, samples, qu, st, stream, 0, need);
-        else if (u == 2) launch_samples<false, 2>(p, geo, mat, samples, qu, st, stream, 0, need);
-        else launch_samples<false, 4>(p, geo, mat, samples, qu, st, stream, 0, need);
+    if (name) *name = v.name;
+#define RTK_CASE(L, U, W)                                                                 \
+    if (v.lds == L && v.unroll == U && v.waves == W) {                                   \
+        launch_samples<L, U, W>(p, geo, mat, samples, qu, st, stream, shmem, need);      \
+        return hipGetLastError();                                                        \
     }
-    return hipGetLastError();
+    RTK_CASE(true, 1, 1) RTK_CASE(true, 2, 1) RTK_CASE(true, 4, 1) RTK_CASE(true, 4, 5)
+    RTK_CASE(false, 1, 1) RTK_CASE(false, 2, 1) RTK_CASE(false, 4, 1) RTK_CASE(false, 4, 5)
+#undef RTK_CASE
+    return hipErrorInvalidValue;
 }
 
 extern "C" hipError_t rtk_launch_reduce(const rtk::ReduceParams* p, const double* samples, double* sums,
