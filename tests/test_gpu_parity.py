@@ -201,3 +201,15 @@ def test_camera_render_api(tmp_path, golden_dir):
     ppm.saveBinary(path)
     data = open(path, "rb").read()
     assert len(data) == 270016 and data.startswith(b"P6\n400 225\n255\n") and data.endswith(b"\n")
+
+
+def test_c_harness_end_to_end(tmp_path):
+    """tools/rt_render_c.c drives the ABI exactly like the Zig shim: its P6 file
+    equals the Python path's fused-RGB8 render of the same preset."""
+    import subprocess
+    exe = os.path.join(os.path.dirname(rtzig.LIB_PATH), "rt_render_c")
+    out = str(tmp_path / "chapter14.ppm")
+    subprocess.run([exe, out, "400", "10", "0xdeadbeef"], check=True, capture_output=True, timeout=300)
+    cam = rtzig.final_scene_camera(width=400, aspect_ratio=16 / 9, spp=10)
+    rgb, _ = gpu_render(cam, cam.scene.world, output="rgb8")
+    assert open(out, "rb").read() == rtzig.encode_p6(rgb, 400, 225)
