@@ -1,0 +1,49 @@
+// rt_bvh.hpp — bounding-volume hierarchy over the sphere list for the BVH walk of the hot path.
+//
+// Why this is exact (DESIGN.md §5 "BVH walk"): HittableList.hit (hittable.zig:64-77) accepts
+// sphere k iff its root t_k (root1 if root1 > t_min, else root2 if root2 > t_min — independent of
+// the running `closest`, because root2 >= root1) is strictly below the running closest.  The scan
+// therefore returns argmin_k t_k with the LOWEST index winning ties.  Any traversal that (1) runs
+// the identical f64 quadratic on every sphere it visits, (2) keeps min t with lowest-index ties, and
+// (3) only skips spheres whose t_k provably exceeds the current closest, returns the same bits.
+// (3) holds because node boxes are f32 boxes padded outward by more than every rounding error of
+// the f32 slab test (see pad rules in rt_bvh.cpp), for every ray origin |o| <= origin_bound.
+#pragma once
+
+#include <cstdint>
+#include <vector>
+
+#include "../../include/rt.h"
+
+namespace rtbvh {
+
+constexpr int kLeafMax = 4;   // spheres per leaf
+constexpr int kMaxDepth = 16; // tree depth bound == per-lane stack size in the kernel
+
+// Internal node: the boxes of both children (f32, padded outward) and their refs.
+// ref >= 0: internal node index; ref < 0: leaf, ~ref = first_slot << 4 | count.
+struct alignas(16) Node {
+    float lo0[3], hi0[3];
+    float lo1[3], hi1[3];
+    int32_t ref0, ref1;
+    int32_t pad[2];
+};  // 64 B
+static_assert(sizeof(Node) == 64, "node layout");
+
+struct Bvh {
+    std::vector<Node> nodes;        // nodes[0] is the root
+    std::vector<uint32_t> slot_to_sphere;  // leaf/always slot -> original sphere index
+    uint32_t n_always = 0;          // slots [0, n_always) are tested for every ray (unboundable spheres)
+    int depth = 0;
+    double origin_bound = 0;        // rays with max|o_i| <= origin_bound are covered by the padding
+    bool ok = false;
+};
+
+// Builds the BVH.  `origin_bound`: bound on |ray origin| components the padding must cover
+// (at least the scene's own extent; the runtime raises it for far-away cameras).
+Bvh build(const rt_sphere* spheres, size_t n, double origin_bound);
+
+// Max |coordinate| of any sphere's bounding box (finite spheres only).
+double scene_extent(const rt_sphere* spheres, size_t n);
+
+}  // namespace rtbvh

@@ -46,6 +46,24 @@ struct KernelParams {
     uint32_t pad_;
 };
 
+// BVH (rt_bvh.hpp): node = both child boxes (f32, padded outward) + child refs; ref >= 0 is a node
+// index, ref < 0 a leaf with ~ref = first_slot << 4 | count.  Slots [0, n_always) hold spheres
+// that are tested for every ray.
+constexpr int kBlockBvh = 512;     // 8 waves; 2 blocks per CU share the LDS budget
+constexpr int kMaxDepthBvh = 16;   // == rtbvh::kMaxDepth: per-lane LDS stack entries
+struct alignas(16) BvhNode {
+    float lo0[3], hi0[3];
+    float lo1[3], hi1[3];
+    int32_t ref0, ref1;
+    int32_t pad[2];
+};
+struct BvhArgs {
+    const BvhNode* nodes;
+    const GeoRec* slot_geo;
+    const uint32_t* slot_id;
+    uint32_t n_nodes, n_slots, n_always, pad;
+};
+
 // Arguments of the ordered reduction: pixel q's running sum += samples[s][q] for s = 0..s_count-1
 // (exactly the reference's sequential `pixelColor += rayColor(ray)`, camera.zig:133-136).
 struct ReduceParams {
@@ -62,5 +80,8 @@ struct ReduceParams {
 extern "C" hipError_t rtk_launch_samples(const rtk::KernelParams* p, const rtk::GeoRec* geo,
                                          const rtk::MatRec* mat, double* samples, void* queue,
                                          void* stats, hipStream_t stream, const char** name);
+extern "C" hipError_t rtk_launch_samples_bvh(const rtk::KernelParams* p, const rtk::BvhArgs* b,
+                                             const rtk::GeoRec* geo, const rtk::MatRec* mat, double* samples,
+                                             void* queue, void* stats, hipStream_t stream, const char** name);
 extern "C" hipError_t rtk_launch_reduce(const rtk::ReduceParams* p, const double* samples,
                                         double* sums, void* out, hipStream_t stream);

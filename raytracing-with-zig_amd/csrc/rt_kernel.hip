@@ -111,21 +111,140 @@ __device__ __forceinline__ uint32_t rank_in(uint64_t mask) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
 }
 
-template <bool kLds, int U, int kWaves>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kWaves))) void sample_kernel(KernelParams p,
-                                                        const GeoRec* __restrict__ geo_g,
-                                                        const MatRec* __restrict__ mat_g,
-                                                        double* __restrict__ samples,
-                                                        unsigned long long* __restrict__ queue,
-                                                        unsigned long long* __restrict__ stats) {
-    extern __shared__ GeoRec lds_geo[];
-    const GeoRec* geo = geo_g;
-    if constexpr (kLds) {
-        for (uint32_t k = threadIdx.x; k < p.n_pad; k += blockDim.x) lds_geo[k] = geo_g[k];
-        __syncthreads();
-        geo = lds_geo;
+// ------------------------------------------------------------------------------------------------
+// Closest-hit walkers.  Both return the ORIGINAL list index of the winning sphere (or -1) and its
+// root in *t_hit, bit-identical to HittableList.hit.
+// ------------------------------------------------------------------------------------------------
+
+// The reference's linear walk over the whole list (hittable.zig:68-74).
+template <int U>
+struct LinearWalker {
+    const GeoRec* __restrict__ geo;
+    uint32_t n_pad;
+    __device__ __forceinline__ int operator()(const Ray& r, double t_min, double t_max, double* t) const {
+        return world_hit<U>(geo, n_pad, r, t_min, t_max, t);
+    }
+};
+
+// BVH walk (rt_bvh.hpp): per-lane, near-child-first, stack in LDS.  Every visited sphere runs the
+// same f64 quadratic as the linear walk; the candidate root of sphere k is
+//   t_k = root1 if t_min < root1, else root2 if t_min < root2   (sphere.zig:38-41),
+// and it wins iff t_k < closest, or t_k == closest and k is lower (the linear scan's first-wins).
+struct BvhWalker {
+    const BvhNode* __restrict__ nodes;
+    const GeoRec* __restrict__ geo;      // slot order
+    const uint32_t* __restrict__ sid;    // slot -> original sphere index
+    uint32_t n_always;
+    int32_t* stack;                      // LDS, element i of this lane at stack[i * kBlockBvh]
+
+    __device__ __forceinline__ void test_slot(uint32_t q, const Ray& r, double a, double t_min, double& closest,
+                                              uint32_t& best, bool& found) const {
+        const GeoRec s = geo[q];
+        const double ocx = s.cx - r.orig.x;
+        const double ocy = s.cy - r.orig.y;
+        const double ocz = s.cz - r.orig.z;
+        const double h = (r.dir.x * ocx + r.dir.y * ocy) + r.dir.z * ocz;
+        const double c = ((ocx * ocx + ocy * ocy) + ocz * ocz) - s.r2;
+        const double disc = h * h - a * c;
+        if (disc >= 0) {
+            const double sq = __builtin_sqrt(disc);
+            double ts = (h - sq) / a;
+            bool cand = t_min < ts;
+            if (!cand) {
+                ts = (h + sq) / a;
+                cand = t_min < ts;
+            }
+            if (cand) {
+                const uint32_t k = sid[q];
+                if (ts < closest || (found && ts == closest && k < best)) {
+                    closest = ts;
+                    best = k;
+                    found = true;
+                }
+            }
+        }
     }
 
+    __device__ __forceinline__ int operator()(const Ray& r, double t_min, double t_max, double* t_hit) const {
+        const double a = len_sq(r.dir);
+        double closest = t_max;
+        uint32_t best = 0;
+        bool found = false;
+        for (uint32_t q = 0; q < n_always; ++q) test_slot(q, r, a, t_min, closest, best, found);
+
+        // f32 ray for the conservative slab tests (error budget: rt_bvh.cpp)
+        const float ox = (float)r.orig.x, oy = (float)r.orig.y, oz = (float)r.orig.z;
+        float dx = (float)r.dir.x, dy = (float)r.dir.y, dz = (float)r.dir.z;
+        if (__builtin_fabsf(dx) < 1e-30f) dx = __builtin_copysignf(1e-30f, dx);
+        if (__builtin_fabsf(dy) < 1e-30f) dy = __builtin_copysignf(1e-30f, dy);
+        if (__builtin_fabsf(dz) < 1e-30f) dz = __builtin_copysignf(1e-30f, dz);
+        const float ix = 1.0f / dx, iy = 1.0f / dy, iz = 1.0f / dz;
+        float lower = (float)t_min;
+        lower = lower - __builtin_fabsf(lower) * 0x1p-20f - 1e-30f;
+        float upper = (float)closest;
+        upper = upper + __builtin_fabsf(upper) * 0x1p-20f;
+
+        int sp = 0;
+        int32_t cur = 0;  // root
+        while (true) {
+            if (cur >= 0) {
+                const BvhNode nd = nodes[cur];
+                float n0, f0, n1, f1;
+                {
+                    const float ax0 = (nd.lo0[0] - ox) * ix, bx0 = (nd.hi0[0] - ox) * ix;
+                    const float ay0 = (nd.lo0[1] - oy) * iy, by0 = (nd.hi0[1] - oy) * iy;
+                    const float az0 = (nd.lo0[2] - oz) * iz, bz0 = (nd.hi0[2] - oz) * iz;
+                    n0 = __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(ax0, bx0), __builtin_fminf(ay0, by0)),
+                                         __builtin_fmaxf(__builtin_fminf(az0, bz0), lower));
+                    f0 = __builtin_fminf(__builtin_fminf(__builtin_fmaxf(ax0, bx0), __builtin_fmaxf(ay0, by0)),
+                                         __builtin_fminf(__builtin_fmaxf(az0, bz0), upper));
+                    const float ax1 = (nd.lo1[0] - ox) * ix, bx1 = (nd.hi1[0] - ox) * ix;
+                    const float ay1 = (nd.lo1[1] - oy) * iy, by1 = (nd.hi1[1] - oy) * iy;
+                    const float az1 = (nd.lo1[2] - oz) * iz, bz1 = (nd.hi1[2] - oz) * iz;
+                    n1 = __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(ax1, bx1), __builtin_fminf(ay1, by1)),
+                                         __builtin_fmaxf(__builtin_fminf(az1, bz1), lower));
+                    f1 = __builtin_fminf(__builtin_fminf(__builtin_fmaxf(ax1, bx1), __builtin_fmaxf(ay1, by1)),
+                                         __builtin_fminf(__builtin_fmaxf(az1, bz1), upper));
+                }
+                const bool h0 = n0 <= f0;
+                const bool h1 = n1 <= f1;
+                if (h0 && h1) {
+                    const bool first0 = n0 <= n1;
+                    stack[sp * kBlockBvh] = first0 ? nd.ref1 : nd.ref0;
+                    ++sp;
+                    cur = first0 ? nd.ref0 : nd.ref1;
+                    continue;
+                }
+                if (h0 || h1) {
+                    cur = h0 ? nd.ref0 : nd.ref1;
+                    continue;
+                }
+            } else {
+                const uint32_t code = (uint32_t)(~cur);
+                const uint32_t first = code >> 4, cnt = code & 15u;
+                for (uint32_t i = 0; i < cnt; ++i) test_slot(first + i, r, a, t_min, closest, best, found);
+                upper = (float)closest;
+                upper = upper + __builtin_fabsf(upper) * 0x1p-20f;
+            }
+            if (sp == 0) break;
+            --sp;
+            cur = stack[sp * kBlockBvh];
+        }
+        *t_hit = closest;
+        return found ? (int)best : -1;
+    }
+};
+
+// ------------------------------------------------------------------------------------------------
+// The path state machine shared by every kernel variant: queue refill + one ray segment per lane
+// per iteration (rayColor's loop body, camera.zig:153-177) + per-sample color stores.
+// `geo_orig` is the geometry in original list order (hit-record center of the winner).
+// ------------------------------------------------------------------------------------------------
+template <class Walker>
+__device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& walk, const GeoRec* __restrict__ geo_orig,
+                                          const MatRec* __restrict__ mat_g, double* __restrict__ samples,
+                                          unsigned long long* __restrict__ queue,
+                                          unsigned long long* __restrict__ stats) {
     const uint32_t W = p.width;
     const uint32_t P = p.n_rows * W;           // pixels per sample layer
     const uint64_t total = (uint64_t)P * p.s_count;
@@ -193,7 +312,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kWaves))
             } else {
                 double t;
                 ++rays;
-                const int k = world_hit<U>(geo, p.n_pad, r, p.t_min, p.t_max, &t);
+                const int k = walk(r, p.t_min, p.t_max, &t);
                 if (k < 0) {
                     // sky gradient (camera.zig:171-177)
                     const double a = 0.5 * (unit(r.dir).y + 1.0);
@@ -201,7 +320,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kWaves))
                     col = att * sky;
                     done = true;
                 } else {
-                    const GeoRec sg = geo[k];
+                    const GeoRec sg = geo_orig[k];
                     const MatRec m = mat_g[k];
                     // hit record (sphere.zig:44-53)
                     const v3 pt = r.orig + muls(r.dir, t);
@@ -267,6 +386,53 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kWaves))
             atomicAdd(&stats[1], (unsigned long long)nsamples);
         }
     }
+}
+
+// Linear-walk kernel: geometry in LDS (kLds) or read by scalar loads from global memory.
+template <bool kLds, int U, int kWaves>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kWaves))) void sample_kernel(
+    KernelParams p, const GeoRec* __restrict__ geo_g, const MatRec* __restrict__ mat_g,
+    double* __restrict__ samples, unsigned long long* __restrict__ queue, unsigned long long* __restrict__ stats) {
+    extern __shared__ GeoRec lds_geo[];
+    const GeoRec* geo = geo_g;
+    if constexpr (kLds) {
+        for (uint32_t k = threadIdx.x; k < p.n_pad; k += blockDim.x) lds_geo[k] = geo_g[k];
+        __syncthreads();
+        geo = lds_geo;
+    }
+    path_loop(p, LinearWalker<U>{geo, p.n_pad}, geo, mat_g, samples, queue, stats);
+}
+
+// BVH-walk kernel: nodes + slot geometry + slot ids staged in LDS (kLdsScene) or read from global
+// memory; the per-lane traversal stack always lives in LDS.
+template <bool kLdsScene>
+__global__ __launch_bounds__(kBlockBvh) void sample_kernel_bvh(KernelParams p, BvhArgs b,
+                                                               const GeoRec* __restrict__ geo_g,
+                                                               const MatRec* __restrict__ mat_g,
+                                                               double* __restrict__ samples,
+                                                               unsigned long long* __restrict__ queue,
+                                                               unsigned long long* __restrict__ stats) {
+    extern __shared__ __align__(16) unsigned char lds_raw[];
+    int32_t* stack = (int32_t*)lds_raw;  // [kMaxDepthBvh][kBlockBvh]
+    unsigned char* scene = lds_raw + (size_t)kMaxDepthBvh * kBlockBvh * sizeof(int32_t);
+    const BvhNode* nodes = b.nodes;
+    const GeoRec* sgeo = b.slot_geo;
+    const uint32_t* sid = b.slot_id;
+    if constexpr (kLdsScene) {
+        BvhNode* ln = (BvhNode*)scene;
+        GeoRec* lg = (GeoRec*)(scene + (size_t)b.n_nodes * sizeof(BvhNode));
+        uint32_t* ls = (uint32_t*)(scene + (size_t)b.n_nodes * sizeof(BvhNode) + (size_t)b.n_slots * sizeof(GeoRec));
+        for (uint32_t k = threadIdx.x; k < b.n_nodes; k += blockDim.x) ln[k] = b.nodes[k];
+        for (uint32_t k = threadIdx.x; k < b.n_slots; k += blockDim.x) {
+            lg[k] = b.slot_geo[k];
+            ls[k] = b.slot_id[k];
+        }
+        __syncthreads();
+        nodes = ln;
+        sgeo = lg;
+        sid = ls;
+    }
+    path_loop(p, BvhWalker{nodes, sgeo, sid, b.n_always, stack + threadIdx.x}, geo_g, mat_g, samples, queue, stats);
 }
 
 template <int kOut>
@@ -388,6 +554,41 @@ extern "C" hipError_t rtk_launch_samples(const rtk::KernelParams* p, const rtk::
     RTK_CASE(false, 1, 1) RTK_CASE(false, 2, 1) RTK_CASE(false, 4, 1) RTK_CASE(false, 4, 5)
 #undef RTK_CASE
     return hipErrorInvalidValue;
+}
+
+extern "C" hipError_t rtk_launch_samples_bvh(const rtk::KernelParams* p, const rtk::BvhArgs* b,
+                                             const rtk::GeoRec* geo, const rtk::MatRec* mat, double* samples,
+                                             void* queue, void* stats, hipStream_t stream, const char** name) {
+    using namespace rtk;
+    const uint64_t total = (uint64_t)p->n_rows * p->width * p->s_count;
+    if (total == 0) return hipSuccess;
+    const size_t stack_bytes = (size_t)kMaxDepthBvh * kBlockBvh * sizeof(int32_t);
+    const size_t scene_bytes = (size_t)b->n_nodes * sizeof(BvhNode) + (size_t)b->n_slots * (sizeof(GeoRec) + 4);
+    // scene in LDS when two blocks (16 waves) still fit a CU's 160 KiB
+    const bool lds_scene = stack_bytes + scene_bytes <= 80 * 1024;
+    const size_t shmem = stack_bytes + (lds_scene ? scene_bytes : 0);
+    const uint64_t need = (total + kBlockBvh - 1) / kBlockBvh;
+    hipError_t e = hipMemsetAsync(queue, 0, sizeof(unsigned long long), stream);
+    if (e != hipSuccess) return e;
+    auto* st = (unsigned long long*)stats;
+    auto* qu = (unsigned long long*)queue;
+    auto launch = [&](auto kernel, const char* nm) -> hipError_t {
+        if (shmem > 64 * 1024) {
+            hipError_t ea = hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shmem);
+            if (ea != hipSuccess) return ea;
+        }
+        int dev = 0, cus = 0, per_cu = 0;
+        if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kBlockBvh, shmem) != hipSuccess || per_cu <= 0)
+            per_cu = 2;
+        const uint64_t cap = (uint64_t)cus * per_cu;
+        const uint32_t blocks = (uint32_t)(need < cap ? need : cap);
+        if (name) *name = nm;
+        hipLaunchKernelGGL(kernel, dim3(blocks), dim3(kBlockBvh), shmem, stream, *p, *b, geo, mat, samples, qu, st);
+        return hipGetLastError();
+    };
+    return lds_scene ? launch(sample_kernel_bvh<true>, "bvh_lds") : launch(sample_kernel_bvh<false>, "bvh_global");
 }
 
 extern "C" hipError_t rtk_launch_reduce(const rtk::ReduceParams* p, const double* samples, double* sums,

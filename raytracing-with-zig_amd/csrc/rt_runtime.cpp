@@ -17,6 +17,7 @@
 #include <vector>
 
 #include "../../include/rt.h"
+#include "rt_bvh.hpp"
 #include "rt_device.h"
 #include "rt_kernel.h"
 
@@ -37,6 +38,15 @@ struct rt_context {
     size_t sums_bytes = 0;
     unsigned long long* d_queue = nullptr;
     const char* last_kernel = "sample_kernel";
+    // BVH over the sphere list (rt_bvh.hpp); empty/!ok => the linear walk
+    std::vector<rt_sphere> spheres;  // host copy (rebuilds for far-away cameras)
+    bool bvh_ok = false;
+    double bvh_origin_bound = 0;
+    rtk::BvhNode* d_nodes = nullptr;
+    rtk::GeoRec* d_slot_geo = nullptr;
+    uint32_t* d_slot_id = nullptr;
+    size_t nodes_bytes = 0, slot_geo_bytes = 0, slot_id_bytes = 0;
+    rtk::BvhArgs bvh{};
     // optional per-kernel timing: event pairs around every sample / reduce launch of the last call
     bool timing = false;
     std::vector<hipEvent_t> events;  // pool; [4c..4c+3] = sample start/stop, reduce start/stop
@@ -113,6 +123,49 @@ int ensure_buffer(void** ptr, size_t* bytes, size_t need) {
     return RT_OK;
 }
 
+// Builds and uploads the BVH for the context's scene, valid for ray origins with |o_i| <= bound.
+int upload_bvh(rt_context* ctx, double bound) {
+    const rtbvh::Bvh bvh = rtbvh::build(ctx->spheres.data(), ctx->spheres.size(), bound);
+    ctx->bvh_ok = bvh.ok;
+    ctx->bvh_origin_bound = bound;
+    if (!bvh.ok) return RT_OK;
+    static_assert(sizeof(rtbvh::Node) == sizeof(rtk::BvhNode), "node layouts differ");
+    const size_t nn = bvh.nodes.size(), ns = bvh.slot_to_sphere.size();
+    std::vector<rtk::GeoRec> sgeo(ns ? ns : 1);
+    for (size_t q = 0; q < ns; q++) {
+        const rt_sphere& sp = ctx->spheres[bvh.slot_to_sphere[q]];
+        const double r = sp.radius > 0 ? sp.radius : 0.0;
+        sgeo[q].cx = sp.center[0];
+        sgeo[q].cy = sp.center[1];
+        sgeo[q].cz = sp.center[2];
+        sgeo[q].r2 = r * r;
+    }
+    int rc = ensure_buffer((void**)&ctx->d_nodes, &ctx->nodes_bytes, nn * sizeof(rtk::BvhNode));
+    if (!rc) rc = ensure_buffer((void**)&ctx->d_slot_geo, &ctx->slot_geo_bytes, sgeo.size() * sizeof(rtk::GeoRec));
+    if (!rc) rc = ensure_buffer((void**)&ctx->d_slot_id, &ctx->slot_id_bytes, (ns ? ns : 1) * sizeof(uint32_t));
+    if (rc) return rc;
+    HIP_CHECK(hipMemcpyAsync(ctx->d_nodes, bvh.nodes.data(), nn * sizeof(rtk::BvhNode), hipMemcpyHostToDevice, ctx->stream));
+    HIP_CHECK(hipMemcpyAsync(ctx->d_slot_geo, sgeo.data(), sgeo.size() * sizeof(rtk::GeoRec), hipMemcpyHostToDevice, ctx->stream));
+    if (ns)
+        HIP_CHECK(hipMemcpyAsync(ctx->d_slot_id, bvh.slot_to_sphere.data(), ns * sizeof(uint32_t), hipMemcpyHostToDevice, ctx->stream));
+    HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    ctx->bvh.nodes = ctx->d_nodes;
+    ctx->bvh.slot_geo = ctx->d_slot_geo;
+    ctx->bvh.slot_id = ctx->d_slot_id;
+    ctx->bvh.n_nodes = (uint32_t)nn;
+    ctx->bvh.n_slots = (uint32_t)ns;
+    ctx->bvh.n_always = bvh.n_always;
+    return RT_OK;
+}
+
+// Walk selection: RTZIG_KERNEL names a linear variant (lds_u*, smem_u*) or "bvh"; default: the
+// BVH walk when it built, else the linear default variant.
+bool use_bvh(const rt_context* ctx) {
+    const char* e = std::getenv("RTZIG_KERNEL");
+    if (e && std::strncmp(e, "bvh", 3) != 0) return false;
+    return ctx->bvh_ok;
+}
+
 rtk::KernelParams make_params(const rt_camera* c, uint32_t fmt, uint32_t row0, uint32_t row_step,
                               uint32_t n_rows, uint32_t n_spheres) {
     rtk::KernelParams p;
@@ -183,6 +236,9 @@ int rt_context_destroy(rt_context* ctx) {
     (void)hipFree(ctx->d_samples);
     (void)hipFree(ctx->d_sums);
     (void)hipFree(ctx->d_queue);
+    (void)hipFree(ctx->d_nodes);
+    (void)hipFree(ctx->d_slot_geo);
+    (void)hipFree(ctx->d_slot_id);
     for (hipEvent_t e : ctx->events) (void)hipEventDestroy(e);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
@@ -228,7 +284,9 @@ int rt_context_set_scene(rt_context* ctx, const rt_sphere* spheres, size_t n) {
     HIP_CHECK(hipMemcpyAsync(ctx->d_mat, mat.data(), n * sizeof(rtk::MatRec), hipMemcpyHostToDevice, ctx->stream));
     HIP_CHECK(hipStreamSynchronize(ctx->stream));
     ctx->n_spheres = (uint32_t)n;
-    return RT_OK;
+    ctx->spheres.assign(spheres, spheres + n);
+    const double extent = rtbvh::scene_extent(spheres, n);
+    return upload_bvh(ctx, extent * (1.0 + 0x1p-20) + 1e-300);
 }
 
 int rt_render_rows_async(rt_context* ctx, const rt_camera* cam, uint32_t output_format, uint32_t row0,
@@ -272,13 +330,27 @@ int rt_render_rows_async(rt_context* ctx, const rt_camera* cam, uint32_t output_
         }
         ctx->timed_chunks = n_chunks;
     }
+    // camera-ray origins (center + defocus disk) must lie inside the BVH padding's origin bound
+    double cam_bound = 0;
+    for (int a = 0; a < 3; a++)
+        cam_bound = std::max(cam_bound, std::fabs(cam->center[a]) + std::fabs(cam->defocus_disk_u[a]) +
+                                            std::fabs(cam->defocus_disk_v[a]));
+    if (ctx->bvh_ok && !(cam_bound <= ctx->bvh_origin_bound)) {
+        rc = upload_bvh(ctx, std::max(cam_bound, ctx->bvh_origin_bound) * 1.01);
+        if (rc) return rc;
+    }
+    const bool bvh = use_bvh(ctx);
     rtk::KernelParams p = make_params(cam, output_format, row0, row_step, n_rows, ctx->n_spheres);
     for (uint32_t c = 0; c < n_chunks; c++) {
         p.s_begin = (uint32_t)(c * s_chunk);
         p.s_count = (uint32_t)std::min<uint64_t>(s_chunk, cam->samples_per_pixel - p.s_begin);
         if (ctx->timing) HIP_CHECK(hipEventRecord(ctx->events[4 * c + 0], s));
-        HIP_CHECK(rtk_launch_samples(&p, ctx->d_geo, ctx->d_mat, ctx->d_samples, ctx->d_queue, d_stats, s,
-                                     &ctx->last_kernel));
+        if (bvh)
+            HIP_CHECK(rtk_launch_samples_bvh(&p, &ctx->bvh, ctx->d_geo, ctx->d_mat, ctx->d_samples, ctx->d_queue,
+                                             d_stats, s, &ctx->last_kernel));
+        else
+            HIP_CHECK(rtk_launch_samples(&p, ctx->d_geo, ctx->d_mat, ctx->d_samples, ctx->d_queue, d_stats, s,
+                                         &ctx->last_kernel));
         if (ctx->timing) HIP_CHECK(hipEventRecord(ctx->events[4 * c + 1], s));
         rtk::ReduceParams rp;
         std::memset(&rp, 0, sizeof rp);

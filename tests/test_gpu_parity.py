@@ -213,3 +213,54 @@ def test_c_harness_end_to_end(tmp_path):
     cam = rtzig.final_scene_camera(width=400, aspect_ratio=16 / 9, spp=10)
     rgb, _ = gpu_render(cam, cam.scene.world, output="rgb8")
     assert open(out, "rb").read() == rtzig.encode_p6(rgb, 400, 225)
+
+
+@pytest.mark.parametrize("variant", ["bvh", "smem_u4", "smem_u1", "lds_u2", "lds_u4"])
+def test_walk_variants_bit_exact(oracle, variant, monkeypatch):
+    """Every closest-hit walk (BVH and the linear list walks) gives oracle B's bits: golden config
+    + the degenerate-materials scene."""
+    monkeypatch.setenv("RTZIG_KERNEL", variant)
+    cam = rtzig.final_scene_camera(width=200, aspect_ratio=16 / 9, spp=6)
+    out, st = gpu_render(cam, cam.scene.world, n_gpus=1)
+    ref, rays = oracle.render_b(cam.cam, cam.scene.world, threads=8)
+    assert np.array_equal(out, ref) and st["rays"] == rays
+    cam = rtzig.chapter13_camera(width=160, spp=8)
+    out, _ = gpu_render(cam, cam.scene.world, n_gpus=1)
+    ref, _ = oracle.render_b(cam.cam, cam.scene.world, threads=8)
+    assert np.array_equal(out, ref)
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_bvh_random_scenes_bit_exact(oracle, seed, monkeypatch):
+    """BVH culling stress: random sphere soups (overlapping, duplicated, tiny and huge spheres,
+    negative radii) from random camera positions; the BVH walk must return the linear scan's bits."""
+    monkeypatch.setenv("RTZIG_KERNEL", "bvh")
+    rng = np.random.default_rng(seed)
+    n = int(rng.integers(2, 300))
+    arr = (RtSphere * (n + 2))()
+    for k in range(n):
+        arr[k] = RtSphere(center=D3(*rng.normal(0, 3, 3)), radius=float(rng.choice([rng.uniform(-0.1, 0.01),
+                          rng.uniform(0.01, 0.5), rng.uniform(0.5, 3)])),
+                          material=int(rng.integers(0, 3)), albedo=D3(*rng.uniform(0, 1, 3)),
+                          fuzz=float(rng.uniform(0, 1.2)), refraction_index=float(rng.uniform(0.5, 2.5)))
+    arr[n] = arr[0]                      # exact duplicate of sphere 0 (tie: index 0 must win)
+    arr[n + 1] = RtSphere(center=D3(0, -1000.5, 0), radius=1000.0, material=0, albedo=D3(0.5, 0.5, 0.5))
+    scene = rtzig.Scene.init(seed)
+    scene.world = arr
+    look_from = tuple(rng.normal(0, 8, 3))
+    cam = (rtzig.Camera.builder(96, 1.5).setScene(scene).setDefocusAngle(float(rng.uniform(0, 3)))
+           .setFocusDist(float(rng.uniform(1, 10))).setViewport(look_from, (0, 0, 0), float(rng.uniform(20, 90)))
+           .setSamplesPerPixel(4).build())
+    out, st = gpu_render(cam, arr, n_gpus=1)
+    ref, rays = oracle.render_b(cam.cam, arr, threads=8)
+    assert np.array_equal(out, ref) and st["rays"] == rays
+
+
+def test_bvh_far_camera_rebuild(oracle, monkeypatch):
+    """A camera far outside the scene's extent raises the BVH padding's origin bound (rebuild)."""
+    monkeypatch.setenv("RTZIG_KERNEL", "bvh")
+    cam = (rtzig.Camera.builder(64, 1.5).setScene(rtzig.Scene.init(5).generateWorld()).setDefocusAngle(0.1)
+           .setFocusDist(5000).setViewport((5000, 300, 4000), (0, 0, 0), 1.0).setSamplesPerPixel(3).build())
+    out, _ = gpu_render(cam, cam.scene.world, n_gpus=1)
+    ref, _ = oracle.render_b(cam.cam, cam.scene.world, threads=8)
+    assert np.array_equal(out, ref)
