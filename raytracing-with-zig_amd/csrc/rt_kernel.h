@@ -43,7 +43,7 @@ struct KernelParams {
     uint32_t row0, row_step, n_rows, n_spheres;
     uint32_t n_pad;  // n_spheres rounded up to kPad (sentinel-padded)
     uint32_t s_begin, s_count;
-    uint32_t pad_;
+    uint32_t prof;  // 1: instrumented build, stats has 8 entries (see rt_context_enable_profile)
 };
 
 // BVH (rt_bvh.hpp): node = both child boxes (f32, padded outward) + child refs; ref >= 0 is a node

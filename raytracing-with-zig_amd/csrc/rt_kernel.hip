@@ -112,6 +112,23 @@ __device__ __forceinline__ uint32_t rank_in(uint64_t mask) {
 }
 
 // ------------------------------------------------------------------------------------------------
+// Optional instrumentation (KernelParams::prof != 0 launches the kProf instantiation): executed
+// sphere tests, BVH node visits and per-wave shader-clock cycles spent in refill / walk / shade.
+// The counts are deterministic functions of the inputs; the cycles are diagnostics only.
+// ------------------------------------------------------------------------------------------------
+template <bool kOn>
+struct Prof {
+    __device__ __forceinline__ void tests(uint32_t) {}
+    __device__ __forceinline__ void visit() {}
+};
+template <>
+struct Prof<true> {
+    uint64_t n_tests = 0, n_visits = 0;
+    __device__ __forceinline__ void tests(uint32_t n) { n_tests += n; }
+    __device__ __forceinline__ void visit() { ++n_visits; }
+};
+
+// ------------------------------------------------------------------------------------------------
 // Closest-hit walkers.  Both return the ORIGINAL list index of the winning sphere (or -1) and its
 // root in *t_hit, bit-identical to HittableList.hit.
 // ------------------------------------------------------------------------------------------------
@@ -121,7 +138,10 @@ template <int U>
 struct LinearWalker {
     const GeoRec* __restrict__ geo;
     uint32_t n_pad;
-    __device__ __forceinline__ int operator()(const Ray& r, double t_min, double t_max, double* t) const {
+    uint32_t n_real;
+    template <class PR>
+    __device__ __forceinline__ int operator()(const Ray& r, double t_min, double t_max, double* t, PR& pr) const {
+        pr.tests(n_real);
         return world_hit<U>(geo, n_pad, r, t_min, t_max, t);
     }
 };
@@ -165,12 +185,14 @@ struct BvhWalker {
         }
     }
 
-    __device__ __forceinline__ int operator()(const Ray& r, double t_min, double t_max, double* t_hit) const {
+    template <class PR>
+    __device__ __forceinline__ int operator()(const Ray& r, double t_min, double t_max, double* t_hit, PR& pr) const {
         const double a = len_sq(r.dir);
         double closest = t_max;
         uint32_t best = 0;
         bool found = false;
         for (uint32_t q = 0; q < n_always; ++q) test_slot(q, r, a, t_min, closest, best, found);
+        pr.tests(n_always);
 
         // f32 ray for the conservative slab tests (error budget: rt_bvh.cpp)
         const float ox = (float)r.orig.x, oy = (float)r.orig.y, oz = (float)r.orig.z;
@@ -188,6 +210,7 @@ struct BvhWalker {
         int32_t cur = 0;  // root
         while (true) {
             if (cur >= 0) {
+                pr.visit();
                 const BvhNode nd = nodes[cur];
                 float n0, f0, n1, f1;
                 {
@@ -223,6 +246,7 @@ struct BvhWalker {
                 const uint32_t code = (uint32_t)(~cur);
                 const uint32_t first = code >> 4, cnt = code & 15u;
                 for (uint32_t i = 0; i < cnt; ++i) test_slot(first + i, r, a, t_min, closest, best, found);
+                pr.tests(cnt);
                 upper = (float)closest;
                 upper = upper + __builtin_fabsf(upper) * 0x1p-20f;
             }
@@ -240,7 +264,7 @@ struct BvhWalker {
 // per iteration (rayColor's loop body, camera.zig:153-177) + per-sample color stores.
 // `geo_orig` is the geometry in original list order (hit-record center of the winner).
 // ------------------------------------------------------------------------------------------------
-template <class Walker>
+template <bool kProf, class Walker>
 __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& walk, const GeoRec* __restrict__ geo_orig,
                                           const MatRec* __restrict__ mat_g, double* __restrict__ samples,
                                           unsigned long long* __restrict__ queue,
@@ -262,8 +286,12 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
     v3 att = mk(1, 1, 1);
     uint32_t bounce = 0;
     uint64_t rays = 0, nsamples = 0;
+    Prof<kProf> pr;
+    uint64_t cyc_refill = 0, cyc_walk = 0, cyc_shade = 0;  // wave-uniform (kProf only)
 
     while (true) {
+        uint64_t t_top = 0;
+        if constexpr (kProf) t_top = __builtin_amdgcn_s_memtime();
         // ---- hand new items to lanes without a path (wave-uniform control flow) ----------------
         uint64_t needy = __ballot(!active);
         while (needy != 0 && !drained) {
@@ -302,6 +330,11 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
             needy = __ballot(!active);
         }
         if (__ballot(active) == 0) break;
+        uint64_t t_walk0 = 0, t_walk1 = 0;
+        if constexpr (kProf) {
+            t_walk0 = __builtin_amdgcn_s_memtime();
+            cyc_refill += t_walk0 - t_top;
+        }
 
         // ---- trace one ray segment per active lane (rayColor's loop body, camera.zig:153-177) --
         if (active) {
@@ -312,7 +345,8 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
             } else {
                 double t;
                 ++rays;
-                const int k = walk(r, p.t_min, p.t_max, &t);
+                const int k = walk(r, p.t_min, p.t_max, &t, pr);
+                if constexpr (kProf) t_walk1 = __builtin_amdgcn_s_memtime();
                 if (k < 0) {
                     // sky gradient (camera.zig:171-177)
                     const double a = 0.5 * (unit(r.dir).y + 1.0);
@@ -373,6 +407,22 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
                 active = false;
             }
         }
+        if constexpr (kProf) {
+            // s_memtime is a scalar op: every lane sees the same stamps; lanes that skipped the
+            // walk this iteration have t_walk1 == 0 and contribute nothing via the max-reduce below
+            const uint64_t t_end = __builtin_amdgcn_s_memtime();
+            uint64_t w1 = t_walk1;
+            for (int off = 32; off > 0; off >>= 1) {
+                const uint64_t o = __shfl_xor(w1, off, 64);
+                w1 = o > w1 ? o : w1;
+            }
+            if (w1 != 0) {
+                cyc_walk += w1 - t_walk0;
+                cyc_shade += t_end - w1;
+            } else {
+                cyc_shade += t_end - t_walk0;
+            }
+        }
     }
 
     if (stats) {
@@ -385,11 +435,25 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
             atomicAdd(&stats[0], (unsigned long long)rays);
             atomicAdd(&stats[1], (unsigned long long)nsamples);
         }
+        if constexpr (kProf) {
+            uint64_t nt = pr.n_tests, nv = pr.n_visits;
+            for (int off = 32; off > 0; off >>= 1) {
+                nt += __shfl_xor(nt, off, 64);
+                nv += __shfl_xor(nv, off, 64);
+            }
+            if (lane == 0) {
+                atomicAdd(&stats[2], (unsigned long long)nt);
+                atomicAdd(&stats[3], (unsigned long long)nv);
+                atomicAdd(&stats[4], (unsigned long long)cyc_refill);
+                atomicAdd(&stats[5], (unsigned long long)cyc_walk);
+                atomicAdd(&stats[6], (unsigned long long)cyc_shade);
+            }
+        }
     }
 }
 
 // Linear-walk kernel: geometry in LDS (kLds) or read by scalar loads from global memory.
-template <bool kLds, int U, int kWaves>
+template <bool kLds, int U, int kWaves, bool kProf>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kWaves))) void sample_kernel(
     KernelParams p, const GeoRec* __restrict__ geo_g, const MatRec* __restrict__ mat_g,
     double* __restrict__ samples, unsigned long long* __restrict__ queue, unsigned long long* __restrict__ stats) {
@@ -400,12 +464,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kWaves))
         __syncthreads();
         geo = lds_geo;
     }
-    path_loop(p, LinearWalker<U>{geo, p.n_pad}, geo, mat_g, samples, queue, stats);
+    path_loop<kProf>(p, LinearWalker<U>{geo, p.n_pad, p.n_spheres}, geo, mat_g, samples, queue, stats);
 }
 
 // BVH-walk kernel: nodes + slot geometry + slot ids staged in LDS (kLdsScene) or read from global
 // memory; the per-lane traversal stack always lives in LDS.
-template <bool kLdsScene>
+template <bool kLdsScene, bool kProf>
 __global__ __launch_bounds__(kBlockBvh) void sample_kernel_bvh(KernelParams p, BvhArgs b,
                                                                const GeoRec* __restrict__ geo_g,
                                                                const MatRec* __restrict__ mat_g,
@@ -432,7 +496,8 @@ __global__ __launch_bounds__(kBlockBvh) void sample_kernel_bvh(KernelParams p, B
         sgeo = lg;
         sid = ls;
     }
-    path_loop(p, BvhWalker{nodes, sgeo, sid, b.n_always, stack + threadIdx.x}, geo_g, mat_g, samples, queue, stats);
+    path_loop<kProf>(p, BvhWalker{nodes, sgeo, sid, b.n_always, stack + threadIdx.x}, geo_g, mat_g, samples, queue,
+                     stats);
 }
 
 template <int kOut>
@@ -499,7 +564,7 @@ uint32_t persistent_blocks(K kernel, size_t shmem) {
 template <bool kLds, int U, int kWaves>
 void launch_samples(const rtk::KernelParams* p, const rtk::GeoRec* geo, const rtk::MatRec* mat, double* samples,
                     unsigned long long* qu, unsigned long long* st, hipStream_t stream, size_t shmem, uint64_t need) {
-    auto kernel = rtk::sample_kernel<kLds, U, kWaves>;
+    auto kernel = p->prof ? rtk::sample_kernel<kLds, U, kWaves, true> : rtk::sample_kernel<kLds, U, kWaves, false>;
     const uint32_t cap = persistent_blocks(kernel, shmem);
     const uint32_t blocks = (uint32_t)(need < cap ? need : cap);
     hipLaunchKernelGGL(kernel, dim3(blocks), dim3(rtk::kBlock), shmem, stream, *p, geo, mat, samples, qu, st);
@@ -588,7 +653,10 @@ extern "C" hipError_t rtk_launch_samples_bvh(const rtk::KernelParams* p, const r
         hipLaunchKernelGGL(kernel, dim3(blocks), dim3(kBlockBvh), shmem, stream, *p, *b, geo, mat, samples, qu, st);
         return hipGetLastError();
     };
-    return lds_scene ? launch(sample_kernel_bvh<true>, "bvh_lds") : launch(sample_kernel_bvh<false>, "bvh_global");
+    if (p->prof)
+        return lds_scene ? launch(sample_kernel_bvh<true, true>, "bvh_lds(prof)")
+                         : launch(sample_kernel_bvh<false, true>, "bvh_global(prof)");
+    return lds_scene ? launch(sample_kernel_bvh<true, false>, "bvh_lds") : launch(sample_kernel_bvh<false, false>, "bvh_global");
 }
 
 extern "C" hipError_t rtk_launch_reduce(const rtk::ReduceParams* p, const double* samples, double* sums,

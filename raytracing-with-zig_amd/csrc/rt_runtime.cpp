@@ -49,6 +49,7 @@ struct rt_context {
     rtk::BvhArgs bvh{};
     // optional per-kernel timing: event pairs around every sample / reduce launch of the last call
     bool timing = false;
+    bool profile = false;  // instrumented kernels: d_stats must hold 8 uint64
     std::vector<hipEvent_t> events;  // pool; [4c..4c+3] = sample start/stop, reduce start/stop
     uint32_t timed_chunks = 0;
 };
@@ -341,6 +342,7 @@ int rt_render_rows_async(rt_context* ctx, const rt_camera* cam, uint32_t output_
     }
     const bool bvh = use_bvh(ctx);
     rtk::KernelParams p = make_params(cam, output_format, row0, row_step, n_rows, ctx->n_spheres);
+    p.prof = ctx->profile && d_stats ? 1u : 0u;
     for (uint32_t c = 0; c < n_chunks; c++) {
         p.s_begin = (uint32_t)(c * s_chunk);
         p.s_count = (uint32_t)std::min<uint64_t>(s_chunk, cam->samples_per_pixel - p.s_begin);
@@ -371,6 +373,12 @@ int rt_context_enable_timing(rt_context* ctx, int enable) {
     if (!ctx) { rt_set_last_error("null context"); return RT_ERR_INVALID; }
     ctx->timing = enable != 0;
     ctx->timed_chunks = 0;
+    return RT_OK;
+}
+
+int rt_context_enable_profile(rt_context* ctx, int enable) {
+    if (!ctx) { rt_set_last_error("null context"); return RT_ERR_INVALID; }
+    ctx->profile = enable != 0;
     return RT_OK;
 }
 

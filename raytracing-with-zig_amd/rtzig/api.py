@@ -203,6 +203,10 @@ class DeviceRenderer:
     def enable_timing(self, enable=True):
         check("rt_context_enable_timing", self.lib.rt_context_enable_timing(self.ctx, int(enable)))
 
+    def enable_profile(self, enable=True):
+        """Instrumented kernels: the stats buffer passed to render_rows_async must hold 8 u64."""
+        check("rt_context_enable_profile", self.lib.rt_context_enable_profile(self.ctx, int(enable)))
+
     def kernel_times(self):
         """(sample_kernel_ms, reduce_kernel_ms) of the last render call (HIP events)."""
         a, b = C.c_double(), C.c_double()

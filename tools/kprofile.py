@@ -1,0 +1,57 @@
+#!/usr/bin/env python3
+"""In-kernel instrumentation report (rt_context_enable_profile): per-ray sphere tests and BVH node
+visits (exact counts) and the wave-cycle split refill / walk / shade, for each walk variant.
+
+    python tools/kprofile.py --spp 100 --variants "bvh smem_u4"
+"""
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "raytracing-with-zig_amd"))
+import torch  # noqa: E402
+
+import rtzig  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--width", type=int, default=1200)
+ap.add_argument("--aspect", type=float, default=1.5)
+ap.add_argument("--spp", type=int, default=100)
+ap.add_argument("--variants", default="bvh smem_u4")
+ap.add_argument("--out", default=None)
+args = ap.parse_args()
+
+cam = rtzig.final_scene_camera(width=args.width, aspect_ratio=args.aspect, spp=args.spp)
+H, W = cam.height, cam.width
+r = rtzig.DeviceRenderer(0)
+r.set_scene(cam.scene.world)
+r.enable_timing(True)
+out = torch.empty((H, W, 3), dtype=torch.float64, device="cuda:0")
+stats = torch.zeros(8, dtype=torch.int64, device="cuda:0")
+res = {"config": f"{W}x{H} {args.spp}spp, {len(cam.scene.world)} spheres", "variants": {}}
+for v in args.variants.split():
+    os.environ["RTZIG_KERNEL"] = v
+    r.enable_profile(False)
+    r.render_rows_async(cam.cam, out.data_ptr())
+    torch.cuda.synchronize()
+    plain_ms, _ = r.kernel_times()
+    r.enable_profile(True)
+    stats.zero_()
+    r.render_rows_async(cam.cam, out.data_ptr(), d_stats_ptr=stats.data_ptr())
+    torch.cuda.synchronize()
+    prof_ms, _ = r.kernel_times()
+    s = [int(x) for x in stats.cpu().tolist()]
+    cyc = s[4] + s[5] + s[6]
+    res["variants"][v] = {
+        "kernel": r.kernel_name(), "sample_kernel_ms": round(plain_ms, 3), "instrumented_ms": round(prof_ms, 3),
+        "rays": s[0], "samples": s[1], "rays_per_sample": round(s[0] / s[1], 4),
+        "sphere_tests_per_ray": round(s[2] / s[0], 3), "node_visits_per_ray": round(s[3] / s[0], 3),
+        "cycle_split": {"refill": round(s[4] / cyc, 4), "walk": round(s[5] / cyc, 4), "shade": round(s[6] / cyc, 4)},
+        "raw": s,
+    }
+    r.enable_profile(False)
+print(json.dumps(res))
+if args.out:
+    json.dump(res, open(args.out, "w"), indent=1)
