@@ -27,6 +27,7 @@
 #include <stdint.h>
 
 #include <cstdlib>
+#include <climits>
 #include <cstring>
 
 #include "rt_device.h"
@@ -208,8 +209,12 @@ struct BvhWalker {
 
         int sp = 0;
         int32_t cur = 0;  // root
-        while (true) {
-            if (cur >= 0) {
+        // while-while (Aila & Laine 2009): every lane advances through internal nodes until it
+        // holds a leaf (or is done); then the lanes with a leaf test its spheres together, so the
+        // f64 leaf work runs with most lanes active instead of whenever any one lane hits a leaf.
+        constexpr int32_t kDone = INT32_MIN;
+        while (cur != kDone) {
+            while (cur >= 0) {
                 pr.visit();
                 const BvhNode nd = nodes[cur];
                 float n0, f0, n1, f1;
@@ -236,23 +241,29 @@ struct BvhWalker {
                     stack[sp * kBlockBvh] = first0 ? nd.ref1 : nd.ref0;
                     ++sp;
                     cur = first0 ? nd.ref0 : nd.ref1;
-                    continue;
-                }
-                if (h0 || h1) {
+                } else if (h0 || h1) {
                     cur = h0 ? nd.ref0 : nd.ref1;
-                    continue;
+                } else if (sp == 0) {
+                    cur = kDone;
+                } else {
+                    --sp;
+                    cur = stack[sp * kBlockBvh];
                 }
-            } else {
+            }
+            if (cur != kDone) {
                 const uint32_t code = (uint32_t)(~cur);
                 const uint32_t first = code >> 4, cnt = code & 15u;
                 for (uint32_t i = 0; i < cnt; ++i) test_slot(first + i, r, a, t_min, closest, best, found);
                 pr.tests(cnt);
                 upper = (float)closest;
                 upper = upper + __builtin_fabsf(upper) * 0x1p-20f;
+                if (sp == 0) {
+                    cur = kDone;
+                } else {
+                    --sp;
+                    cur = stack[sp * kBlockBvh];
+                }
             }
-            if (sp == 0) break;
-            --sp;
-            cur = stack[sp * kBlockBvh];
         }
         *t_hit = closest;
         return found ? (int)best : -1;
@@ -364,12 +375,17 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
                     const v3 albedo = mk(m.albedo[0], m.albedo[1], m.albedo[2]);
                     v3 dir;
                     done = false;
+                    // Lambertian and Metal each draw exactly one Vec.randomUnitVec and nothing
+                    // else, so one shared rejection loop serves both (one divergent loop per wave
+                    // instead of two) with the same draws in the same order.
+                    v3 ruv = mk(0, 0, 0);
+                    if (m.kind <= 1) ruv = random_unit_vec(g);
                     if (m.kind == 0) {  // Lambertian.scatter (material.zig:27-39)
-                        dir = nrm + random_unit_vec(g);
+                        dir = nrm + ruv;
                         if (near_zero(dir)) dir = nrm;
                         att = att * albedo;
                     } else if (m.kind == 1) {  // Metal.scatter (material.zig:55-68)
-                        dir = unit(reflect(r.dir, nrm)) + muls(random_unit_vec(g), m.fuzz);
+                        dir = unit(reflect(r.dir, nrm)) + muls(ruv, m.fuzz);
                         if (!(dot(dir, nrm) > 0)) {
                             done = true;  // absorbed -> black
                         } else {
