@@ -67,10 +67,13 @@ struct Builder {
         }
     }
 
+    // Leaves are padded to exactly kLeafMax slots with sentinels (kSentinel: never-hit geometry,
+    // see rt_kernel.h), so the kernel tests every leaf with one fixed, unrolled block.
     int32_t leaf(size_t b, size_t e) {
         const uint32_t first = slot_base + (uint32_t)slots.size();
         for (size_t i = b; i < e; i++) slots.push_back(prims[i].sphere);
-        return ~(int32_t)((first << 4) | (uint32_t)(e - b));
+        for (size_t i = e - b; i < (size_t)kLeafMax; i++) slots.push_back(kSentinel);
+        return ~(int32_t)((first << 4) | (uint32_t)kLeafMax);
     }
 
     // returns the ref of the subtree over prims[b, e) at `depth` (root = 1)
@@ -196,7 +199,7 @@ Bvh build(const rt_sphere* spheres, size_t n, double origin_bound) {
     if (m <= (size_t)kLeafMax) {
         // root with one leaf holding everything and one empty leaf (count 0)
         B.nodes.emplace_back();
-        const int32_t r0 = m ? B.leaf(0, m) : ~(int32_t)0;
+        const int32_t r0 = B.leaf(0, m);
         Node& nd = B.nodes[0];
         if (m) {
             B.set_box(nd.lo0, nd.hi0, 0, m);
@@ -205,7 +208,7 @@ Bvh build(const rt_sphere* spheres, size_t n, double origin_bound) {
         }
         for (int a = 0; a < 3; a++) nd.lo1[a] = nd.hi1[a] = 3e38f;
         nd.ref0 = r0;
-        nd.ref1 = ~(int32_t)0;  // empty leaf: first 0, count 0
+        nd.ref1 = B.leaf(0, 0);  // all-sentinel leaf
         nd.pad[0] = nd.pad[1] = 0;
         B.max_depth = 2;
     } else {

@@ -19,6 +19,7 @@ namespace rtbvh {
 
 constexpr int kLeafMax = 4;   // spheres per leaf
 constexpr int kMaxDepth = 16; // tree depth bound == per-lane stack size in the kernel
+constexpr uint32_t kSentinel = 0xffffffffu;  // slot_to_sphere value of a padding slot
 
 // Internal node: the boxes of both children (f32, padded outward) and their refs.
 // ref >= 0: internal node index; ref < 0: leaf, ~ref = first_slot << 4 | count.

@@ -51,6 +51,7 @@ struct KernelParams {
 // that are tested for every ray.
 constexpr int kBlockBvh = 512;     // 8 waves; 2 blocks per CU share the LDS budget
 constexpr int kMaxDepthBvh = 16;   // == rtbvh::kMaxDepth: per-lane LDS stack entries
+constexpr int kLeafBvh = 4;        // == rtbvh::kLeafMax: slots per (sentinel-padded) leaf
 struct alignas(16) BvhNode {
     float lo0[3], hi0[3];
     float lo1[3], hi1[3];

@@ -167,21 +167,25 @@ struct BvhWalker {
         const double h = (r.dir.x * ocx + r.dir.y * ocy) + r.dir.z * ocz;
         const double c = ((ocx * ocx + ocy * ocy) + ocz * ocz) - s.r2;
         const double disc = h * h - a * c;
-        if (disc >= 0) {
-            const double sq = __builtin_sqrt(disc);
-            double ts = (h - sq) / a;
-            bool cand = t_min < ts;
-            if (!cand) {
-                ts = (h + sq) / a;
-                cand = t_min < ts;
-            }
-            if (cand) {
-                const uint32_t k = sid[q];
-                if (ts < closest || (found && ts == closest && k < best)) {
-                    closest = ts;
-                    best = k;
-                    found = true;
-                }
+        if (disc >= 0) candidate(q, h, disc, a, t_min, closest, best, found);
+    }
+
+    // root selection of sphere.zig:35-41 for a slot with disc >= 0, then the first-wins argmin
+    __device__ __forceinline__ void candidate(uint32_t q, double h, double disc, double a, double t_min,
+                                              double& closest, uint32_t& best, bool& found) const {
+        const double sq = __builtin_sqrt(disc);
+        double ts = (h - sq) / a;
+        bool cand = t_min < ts;
+        if (!cand) {
+            ts = (h + sq) / a;
+            cand = t_min < ts;
+        }
+        if (cand) {
+            const uint32_t k = sid[q];
+            if (ts < closest || (found && ts == closest && k < best)) {
+                closest = ts;
+                best = k;
+                found = true;
             }
         }
     }
@@ -236,13 +240,16 @@ struct BvhWalker {
                 }
                 const bool h0 = n0 <= f0;
                 const bool h1 = n1 <= f1;
-                if (h0 && h1) {
-                    const bool first0 = n0 <= n1;
-                    stack[sp * kBlockBvh] = first0 ? nd.ref1 : nd.ref0;
-                    ++sp;
-                    cur = first0 ? nd.ref0 : nd.ref1;
-                } else if (h0 || h1) {
-                    cur = h0 ? nd.ref0 : nd.ref1;
+                // both hit: descend into the nearer child and push the farther one (the store
+                // always happens; it only counts when sp advances); one hit: descend; none: pop
+                const bool first0 = n0 <= n1;
+                const int32_t near_ref = first0 ? nd.ref0 : nd.ref1;
+                const int32_t far_ref = first0 ? nd.ref1 : nd.ref0;
+                stack[sp * kBlockBvh] = far_ref;
+                const bool both = h0 && h1;
+                sp += both ? 1 : 0;
+                if (h0 || h1) {
+                    cur = both ? near_ref : (h0 ? nd.ref0 : nd.ref1);
                 } else if (sp == 0) {
                     cur = kDone;
                 } else {
@@ -251,10 +258,25 @@ struct BvhWalker {
                 }
             }
             if (cur != kDone) {
-                const uint32_t code = (uint32_t)(~cur);
-                const uint32_t first = code >> 4, cnt = code & 15u;
-                for (uint32_t i = 0; i < cnt; ++i) test_slot(first + i, r, a, t_min, closest, best, found);
-                pr.tests(cnt);
+                // leaf: exactly kLeafBvh slots (sentinel-padded); the four discriminant chains
+                // are independent, the candidate updates then run in slot order
+                const uint32_t first = ((uint32_t)(~cur)) >> 4;
+                double h[kLeafBvh], disc[kLeafBvh];
+#pragma unroll
+                for (int u = 0; u < kLeafBvh; ++u) {
+                    const GeoRec s = geo[first + u];
+                    const double ocx = s.cx - r.orig.x;
+                    const double ocy = s.cy - r.orig.y;
+                    const double ocz = s.cz - r.orig.z;
+                    h[u] = (r.dir.x * ocx + r.dir.y * ocy) + r.dir.z * ocz;
+                    const double c = ((ocx * ocx + ocy * ocy) + ocz * ocz) - s.r2;
+                    disc[u] = h[u] * h[u] - a * c;
+                }
+#pragma unroll
+                for (int u = 0; u < kLeafBvh; ++u) {
+                    if (disc[u] >= 0) candidate(first + u, h[u], disc[u], a, t_min, closest, best, found);
+                }
+                pr.tests(kLeafBvh);
                 upper = (float)closest;
                 upper = upper + __builtin_fabsf(upper) * 0x1p-20f;
                 if (sp == 0) {

@@ -131,9 +131,15 @@ int upload_bvh(rt_context* ctx, double bound) {
     ctx->bvh_origin_bound = bound;
     if (!bvh.ok) return RT_OK;
     static_assert(sizeof(rtbvh::Node) == sizeof(rtk::BvhNode), "node layouts differ");
+    static_assert(rtbvh::kLeafMax == rtk::kLeafBvh && rtbvh::kMaxDepth == rtk::kMaxDepthBvh, "BVH constants differ");
     const size_t nn = bvh.nodes.size(), ns = bvh.slot_to_sphere.size();
     std::vector<rtk::GeoRec> sgeo(ns ? ns : 1);
     for (size_t q = 0; q < ns; q++) {
+        if (bvh.slot_to_sphere[q] == rtbvh::kSentinel) {  // never-hit padding slot
+            sgeo[q].cx = sgeo[q].cy = sgeo[q].cz = 0.0;
+            sgeo[q].r2 = -std::numeric_limits<double>::infinity();
+            continue;
+        }
         const rt_sphere& sp = ctx->spheres[bvh.slot_to_sphere[q]];
         const double r = sp.radius > 0 ? sp.radius : 0.0;
         sgeo[q].cx = sp.center[0];
