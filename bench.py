@@ -34,6 +34,7 @@ METRIC = "Msamples/sec (pixels×spp/s) on final-render scene; achieved HBM GB/s 
 FP64_VALU_PEAK_TFLOPS = 78.6   # MI355X vector FP64 (spec), = unpacked FP32 vector rate
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E (spec), MI355X_MICROARCH.md
 FLOPS_PER_TEST = 17            # oc(3) + h(5) + |oc|^2(5) + -r^2(1) + h^2-a*c(3), SURVEY §8(d)
+F32_FLOPS_PER_VISIT = 24       # BVH node visit: 2 child boxes x 3 axes x 2 planes x (sub + mul), f32
 
 
 def log(*a):
@@ -133,6 +134,16 @@ def main():
 
     for _ in range(args.warmup):
         frame()
+    # one untimed instrumented frame: exact executed-work counts (sphere tests, BVH node visits)
+    pstats = torch.zeros(8, dtype=torch.int64, device=dev)
+    if n_rows:
+        renderer.enable_profile(True)
+        renderer.render_rows_async(cam.cam, out.data_ptr(), row0=row0, row_step=step, n_rows=n_rows,
+                                   output=args.output, d_stats_ptr=pstats.data_ptr(),
+                                   stream_ptr=stream.cuda_stream)
+        torch.cuda.synchronize()
+        renderer.enable_profile(False)
+    prof = [int(x) for x in pstats.cpu().tolist()]
     stats.zero_()
 
     if world > 1:
@@ -160,8 +171,14 @@ def main():
         value = total_samples / elapsed_max / 1e6
         k_avg_s = float(np.mean([a for a, _ in kernel_ms])) / 1e3   # sample_kernel only
         r_avg_ms = float(np.mean([b for _, b in kernel_ms]))
-        flops = FLOPS_PER_TEST * n_spheres * rays_per_launch
-        achieved_tf = flops / k_avg_s / 1e12
+        # executed work of the dominant kernel (exact counts from the instrumented frame):
+        # f64 sphere tests (17 FLOP each) + f32 BVH box tests (12 FLOP each); f32 VALU runs at twice
+        # the f64 rate on gfx950, so f32 FLOPs count half against the FP64 peak
+        tests, visits = prof[2], prof[3]
+        f64_flops = FLOPS_PER_TEST * tests
+        f32_flops = F32_FLOPS_PER_VISIT * visits
+        achieved_tf = (f64_flops + f32_flops / 2) / k_avg_s / 1e12
+        ref_equiv_tf = FLOPS_PER_TEST * n_spheres * rays_per_launch / k_avg_s / 1e12
         # sample_kernel HBM bytes: one 24-B f64 color per sample written (the reduce kernel reads
         # them back: +24 B/sample, + the framebuffer)
         alg_bytes = n_rows * W * spp * 24
@@ -193,8 +210,14 @@ def main():
                 "unit": "TFLOP/s",
                 "frac": round(achieved_tf / FP64_VALU_PEAK_TFLOPS, 4),
                 "traffic": traffic,
-                "work": f"{FLOPS_PER_TEST} FLOP x {n_spheres} spheres x {rays_per_launch:.0f} rays "
-                        f"per launch (rank 0, {n_rows} rows)",
+                "work": f"executed per launch (rank 0, {n_rows} rows): {tests} exact f64 ray-sphere "
+                        f"tests x {FLOPS_PER_TEST} FLOP + {visits} BVH node visits x "
+                        f"{F32_FLOPS_PER_VISIT} f32 FLOP (counted at 1/2); {rays_per_launch:.0f} rays",
+                "sphere_tests_per_ray": round(tests / max(1, prof[0]), 3),
+                "node_visits_per_ray": round(visits / max(1, prof[0]), 3),
+                "reference_equivalent_TFLOPs": round(ref_equiv_tf, 3),
+                "reference_equivalent_note": f"17 FLOP x {n_spheres} spheres x rays / t: the work the "
+                                             "reference's linear list walk would do for the same bits",
                 "kernel_ms_avg": round(k_avg_s * 1e3, 3),
                 "reduce_kernel_ms_avg": round(r_avg_ms, 3),
             },
