@@ -347,8 +347,10 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
                 if (rk < take) {
                     item = cur + rk;
                     active = true;
-                    const uint32_t s_local = (uint32_t)(item / P);
-                    const uint32_t q = (uint32_t)(item - (uint64_t)s_local * P);
+                    // items per launch < 2^32 (host-side chunking): 32-bit index math
+                    const uint32_t it32 = (uint32_t)item;
+                    const uint32_t s_local = it32 / P;
+                    const uint32_t q = it32 - s_local * P;
                     const uint32_t row_local = q / W;
                     const uint32_t i = q - row_local * W;
                     const uint32_t j = p.row0 + row_local * p.row_step;

@@ -77,8 +77,8 @@ int validate_camera(const rt_camera* c) {
         rt_set_last_error("samples_per_pixel must be > 0");
         return RT_ERR_INVALID;
     }
-    if ((uint64_t)c->image_width * c->image_height > (1ULL << 32)) {
-        rt_set_last_error("image larger than 2^32 pixels");
+    if ((uint64_t)c->image_width * c->image_height >= (1ULL << 32)) {
+        rt_set_last_error("image must have fewer than 2^32 pixels");
         return RT_ERR_INVALID;
     }
     return RT_OK;
@@ -320,6 +320,7 @@ int rt_render_rows_async(rt_context* ctx, const rt_camera* cam, uint32_t output_
     uint64_t s_chunk = workspace_budget() / layer;
     if (s_chunk < 1) s_chunk = 1;
     if (s_chunk > cam->samples_per_pixel) s_chunk = cam->samples_per_pixel;
+    if (s_chunk * P > 0xffffffffULL) s_chunk = 0xffffffffULL / P;  // kernel item index is 32-bit
     const uint32_t n_chunks = (uint32_t)((cam->samples_per_pixel + s_chunk - 1) / s_chunk);
     rc = ensure_buffer((void**)&ctx->d_samples, &ctx->samples_bytes, s_chunk * layer);
     if (!rc && n_chunks > 1) rc = ensure_buffer((void**)&ctx->d_sums, &ctx->sums_bytes, layer);
