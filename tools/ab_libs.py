@@ -1,0 +1,60 @@
+#!/usr/bin/env python3
+"""In-process A/B of whole library builds (cdna guide rule 24): loads several copies of
+librtzig.so (built from different revisions by tools/build_variant.sh), renders the same frame
+with each in interleaved rounds, checks the outputs are bit-identical, and reports the sample
+kernel's median HIP-event time per build.
+
+    python tools/ab_libs.py ab/base.so ab/new.so --spp 100 --rounds 5
+"""
+import argparse
+import ctypes as C
+import json
+import os
+import statistics
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "raytracing-with-zig_amd"))
+import torch  # noqa: E402
+
+import rtzig  # noqa: E402
+from rtzig import lib as rlib  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("libs", nargs="+")
+ap.add_argument("--width", type=int, default=1200)
+ap.add_argument("--aspect", type=float, default=1.5)
+ap.add_argument("--spp", type=int, default=100)
+ap.add_argument("--rounds", type=int, default=5)
+args = ap.parse_args()
+
+cam = rtzig.final_scene_camera(width=args.width, aspect_ratio=args.aspect, spp=args.spp)
+H, W = cam.height, cam.width
+out = torch.empty((H, W, 3), dtype=torch.float64, device="cuda:0")
+runs = []
+for path in args.libs:
+    L = C.CDLL(os.path.abspath(path))
+    rlib._declare(L)
+    ctx = C.c_void_p()
+    assert L.rt_context_create(0, C.byref(ctx)) == 0, L.rt_last_error()
+    assert L.rt_context_set_scene(ctx, cam.scene.world, len(cam.scene.world)) == 0, L.rt_last_error()
+    assert L.rt_context_enable_timing(ctx, 1) == 0
+    runs.append((path, L, ctx))
+times = {p: [] for p, _, _ in runs}
+ref = None
+for rnd in range(args.rounds + 1):
+    for path, L, ctx in runs:
+        rc = L.rt_render_rows_async(ctx, C.byref(cam.cam), 0, 0, 1, H, C.c_void_p(out.data_ptr()), None, None)
+        assert rc == 0, L.rt_last_error()
+        torch.cuda.synchronize()
+        a, b = C.c_double(), C.c_double()
+        assert L.rt_context_kernel_times(ctx, C.byref(a), C.byref(b)) == 0
+        img = out.cpu()
+        if ref is None:
+            ref = img
+        assert torch.equal(img, ref), f"{path} output differs"
+        if rnd > 0:
+            times[path].append(a.value)
+res = {p: {"median_ms": round(statistics.median(t), 3), "min_ms": round(min(t), 3),
+           "Msamples_s": round(W * H * args.spp / statistics.median(t) / 1e3, 1)} for p, t in times.items()}
+print(json.dumps({"config": f"{W}x{H} {args.spp}spp", "results": res}))
