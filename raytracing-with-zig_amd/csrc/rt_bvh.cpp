@@ -70,10 +70,10 @@ struct Builder {
     // Leaves are padded to exactly kLeafMax slots with sentinels (kSentinel: never-hit geometry,
     // see rt_kernel.h), so the kernel tests every leaf with one fixed, unrolled block.
     int32_t leaf(size_t b, size_t e) {
-        const uint32_t first = slot_base + (uint32_t)slots.size();
+        const uint32_t index = (uint32_t)(slots.size() / kLeafMax);
         for (size_t i = b; i < e; i++) slots.push_back(prims[i].sphere);
         for (size_t i = e - b; i < (size_t)kLeafMax; i++) slots.push_back(kSentinel);
-        return ~(int32_t)((first << 4) | (uint32_t)kLeafMax);
+        return ~(int32_t)index;
     }
 
     // returns the ref of the subtree over prims[b, e) at `depth` (root = 1)

@@ -22,7 +22,8 @@ constexpr int kMaxDepth = 16; // tree depth bound == per-lane stack size in the 
 constexpr uint32_t kSentinel = 0xffffffffu;  // slot_to_sphere value of a padding slot
 
 // Internal node: the boxes of both children (f32, padded outward) and their refs.
-// ref >= 0: internal node index; ref < 0: leaf, ~ref = first_slot << 4 | count.
+// ref >= 0: internal node index; ref < 0: leaf index ~ref.  Leaf L holds slots
+// [n_always + 4L, n_always + 4L + 4) (sentinel-padded to exactly kLeafMax).
 struct alignas(16) Node {
     float lo0[3], hi0[3];
     float lo1[3], hi1[3];

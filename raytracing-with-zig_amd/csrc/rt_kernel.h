@@ -46,9 +46,10 @@ struct KernelParams {
     uint32_t prof;  // 1: instrumented build, stats has 8 entries (see rt_context_enable_profile)
 };
 
-// BVH (rt_bvh.hpp): node = both child boxes (f32, padded outward) + child refs; ref >= 0 is a node
-// index, ref < 0 a leaf with ~ref = first_slot << 4 | count.  Slots [0, n_always) hold spheres
-// that are tested for every ray.
+// BVH (rt_bvh.hpp).  Node = both child boxes (f32, padded outward) + child refs; ref >= 0 is a
+// node index, ref < 0 the leaf ~ref.  Strides are ODD multiples of 16 B (node 80 B = 5 x 16, leaf
+// 144 B = 9 x 16) so that the per-lane random gathers (ds_read_b128) spread over all 16 bank slots
+// of the 256-B LDS row instead of piling onto 4 (64-B stride) or 2 (128-B stride) of them.
 constexpr int kBlockBvh = 512;     // 8 waves; 2 blocks per CU share the LDS budget
 constexpr int kMaxDepthBvh = 16;   // == rtbvh::kMaxDepth: per-lane LDS stack entries
 constexpr int kLeafBvh = 4;        // == rtbvh::kLeafMax: slots per (sentinel-padded) leaf
@@ -56,13 +57,22 @@ struct alignas(16) BvhNode {
     float lo0[3], hi0[3];
     float lo1[3], hi1[3];
     int32_t ref0, ref1;
-    int32_t pad[2];
+    int32_t pad[6];
+};  // 80 B
+struct alignas(16) LeafGeo {
+    double cx, cy, cz, r2;    // as GeoRec, 16-B aligned so that a leaf packs to 144 B
 };
+struct alignas(16) BvhLeaf {
+    LeafGeo g[kLeafBvh];      // slot geometry (sentinels: {0,0,0,-inf})
+    uint32_t sid[kLeafBvh];   // original sphere index per slot (0xffffffff for sentinels)
+};  // 144 B
+static_assert(sizeof(BvhNode) == 80 && sizeof(BvhLeaf) == 144, "BVH layouts");
 struct BvhArgs {
     const BvhNode* nodes;
-    const GeoRec* slot_geo;
-    const uint32_t* slot_id;
-    uint32_t n_nodes, n_slots, n_always, pad;
+    const BvhLeaf* leaves;
+    const GeoRec* always_geo;    // spheres tested for every ray (unboundable)
+    const uint32_t* always_sid;
+    uint32_t n_nodes, n_leaves, n_always, pad;
 };
 
 // Arguments of the ordered reduction: pixel q's running sum += samples[s][q] for s = 0..s_count-1

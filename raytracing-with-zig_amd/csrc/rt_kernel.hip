@@ -153,26 +153,28 @@ struct LinearWalker {
 // and it wins iff t_k < closest, or t_k == closest and k is lower (the linear scan's first-wins).
 struct BvhWalker {
     const BvhNode* __restrict__ nodes;
-    const GeoRec* __restrict__ geo;      // slot order
-    const uint32_t* __restrict__ sid;    // slot -> original sphere index
+    const BvhLeaf* __restrict__ leaves;
+    const GeoRec* __restrict__ ageo;     // always-list geometry
+    const uint32_t* __restrict__ asid;   // always-list original indices
     uint32_t n_always;
     int32_t* stack;                      // LDS, element i of this lane at stack[i * kBlockBvh]
 
-    __device__ __forceinline__ void test_slot(uint32_t q, const Ray& r, double a, double t_min, double& closest,
-                                              uint32_t& best, bool& found) const {
-        const GeoRec s = geo[q];
+    // always-list sphere q
+    __device__ __forceinline__ void test_always(uint32_t q, const Ray& r, double a, double t_min, double& closest,
+                                                uint32_t& best, bool& found) const {
+        const GeoRec s = ageo[q];
         const double ocx = s.cx - r.orig.x;
         const double ocy = s.cy - r.orig.y;
         const double ocz = s.cz - r.orig.z;
         const double h = (r.dir.x * ocx + r.dir.y * ocy) + r.dir.z * ocz;
         const double c = ((ocx * ocx + ocy * ocy) + ocz * ocz) - s.r2;
         const double disc = h * h - a * c;
-        if (disc >= 0) candidate(q, h, disc, a, t_min, closest, best, found);
+        if (disc >= 0) candidate(asid[q], h, disc, a, t_min, closest, best, found);
     }
 
-    // root selection of sphere.zig:35-41 for a slot with disc >= 0, then the first-wins argmin
-    __device__ __forceinline__ void candidate(uint32_t q, double h, double disc, double a, double t_min,
-                                              double& closest, uint32_t& best, bool& found) const {
+    // root selection of sphere.zig:35-41 for a sphere with disc >= 0, then the first-wins argmin
+    __device__ __forceinline__ static void candidate(uint32_t k, double h, double disc, double a, double t_min,
+                                                     double& closest, uint32_t& best, bool& found) {
         const double sq = __builtin_sqrt(disc);
         double ts = (h - sq) / a;
         bool cand = t_min < ts;
@@ -180,13 +182,10 @@ struct BvhWalker {
             ts = (h + sq) / a;
             cand = t_min < ts;
         }
-        if (cand) {
-            const uint32_t k = sid[q];
-            if (ts < closest || (found && ts == closest && k < best)) {
-                closest = ts;
-                best = k;
-                found = true;
-            }
+        if (cand && (ts < closest || (found && ts == closest && k < best))) {
+            closest = ts;
+            best = k;
+            found = true;
         }
     }
 
@@ -196,7 +195,7 @@ struct BvhWalker {
         double closest = t_max;
         uint32_t best = 0;
         bool found = false;
-        for (uint32_t q = 0; q < n_always; ++q) test_slot(q, r, a, t_min, closest, best, found);
+        for (uint32_t q = 0; q < n_always; ++q) test_always(q, r, a, t_min, closest, best, found);
         pr.tests(n_always);
 
         // f32 ray for the conservative slab tests (error budget: rt_bvh.cpp)
@@ -260,11 +259,11 @@ struct BvhWalker {
             if (cur != kDone) {
                 // leaf: exactly kLeafBvh slots (sentinel-padded); the four discriminant chains
                 // are independent, the candidate updates then run in slot order
-                const uint32_t first = ((uint32_t)(~cur)) >> 4;
+                const BvhLeaf* lf = leaves + (uint32_t)(~cur);
                 double h[kLeafBvh], disc[kLeafBvh];
 #pragma unroll
                 for (int u = 0; u < kLeafBvh; ++u) {
-                    const GeoRec s = geo[first + u];
+                    const LeafGeo s = lf->g[u];
                     const double ocx = s.cx - r.orig.x;
                     const double ocy = s.cy - r.orig.y;
                     const double ocz = s.cz - r.orig.z;
@@ -274,7 +273,7 @@ struct BvhWalker {
                 }
 #pragma unroll
                 for (int u = 0; u < kLeafBvh; ++u) {
-                    if (disc[u] >= 0) candidate(first + u, h[u], disc[u], a, t_min, closest, best, found);
+                    if (disc[u] >= 0) candidate(lf->sid[u], h[u], disc[u], a, t_min, closest, best, found);
                 }
                 pr.tests(kLeafBvh);
                 upper = (float)closest;
@@ -520,24 +519,18 @@ __global__ __launch_bounds__(kBlockBvh) void sample_kernel_bvh(KernelParams p, B
     int32_t* stack = (int32_t*)lds_raw;  // [kMaxDepthBvh][kBlockBvh]
     unsigned char* scene = lds_raw + (size_t)kMaxDepthBvh * kBlockBvh * sizeof(int32_t);
     const BvhNode* nodes = b.nodes;
-    const GeoRec* sgeo = b.slot_geo;
-    const uint32_t* sid = b.slot_id;
+    const BvhLeaf* leaves = b.leaves;
     if constexpr (kLdsScene) {
         BvhNode* ln = (BvhNode*)scene;
-        GeoRec* lg = (GeoRec*)(scene + (size_t)b.n_nodes * sizeof(BvhNode));
-        uint32_t* ls = (uint32_t*)(scene + (size_t)b.n_nodes * sizeof(BvhNode) + (size_t)b.n_slots * sizeof(GeoRec));
+        BvhLeaf* ll = (BvhLeaf*)(scene + (size_t)b.n_nodes * sizeof(BvhNode));
         for (uint32_t k = threadIdx.x; k < b.n_nodes; k += blockDim.x) ln[k] = b.nodes[k];
-        for (uint32_t k = threadIdx.x; k < b.n_slots; k += blockDim.x) {
-            lg[k] = b.slot_geo[k];
-            ls[k] = b.slot_id[k];
-        }
+        for (uint32_t k = threadIdx.x; k < b.n_leaves; k += blockDim.x) ll[k] = b.leaves[k];
         __syncthreads();
         nodes = ln;
-        sgeo = lg;
-        sid = ls;
+        leaves = ll;
     }
-    path_loop<kProf>(p, BvhWalker{nodes, sgeo, sid, b.n_always, stack + threadIdx.x}, geo_g, mat_g, samples, queue,
-                     stats);
+    path_loop<kProf>(p, BvhWalker{nodes, leaves, b.always_geo, b.always_sid, b.n_always, stack + threadIdx.x}, geo_g,
+                     mat_g, samples, queue, stats);
 }
 
 template <int kOut>
@@ -668,7 +661,7 @@ extern "C" hipError_t rtk_launch_samples_bvh(const rtk::KernelParams* p, const r
     const uint64_t total = (uint64_t)p->n_rows * p->width * p->s_count;
     if (total == 0) return hipSuccess;
     const size_t stack_bytes = (size_t)kMaxDepthBvh * kBlockBvh * sizeof(int32_t);
-    const size_t scene_bytes = (size_t)b->n_nodes * sizeof(BvhNode) + (size_t)b->n_slots * (sizeof(GeoRec) + 4);
+    const size_t scene_bytes = (size_t)b->n_nodes * sizeof(BvhNode) + (size_t)b->n_leaves * sizeof(BvhLeaf);
     // scene in LDS when two blocks (16 waves) still fit a CU's 160 KiB
     const bool lds_scene = stack_bytes + scene_bytes <= 80 * 1024;
     const size_t shmem = stack_bytes + (lds_scene ? scene_bytes : 0);

@@ -43,9 +43,10 @@ struct rt_context {
     bool bvh_ok = false;
     double bvh_origin_bound = 0;
     rtk::BvhNode* d_nodes = nullptr;
-    rtk::GeoRec* d_slot_geo = nullptr;
-    uint32_t* d_slot_id = nullptr;
-    size_t nodes_bytes = 0, slot_geo_bytes = 0, slot_id_bytes = 0;
+    rtk::BvhLeaf* d_leaves = nullptr;
+    rtk::GeoRec* d_always_geo = nullptr;
+    uint32_t* d_always_sid = nullptr;
+    size_t nodes_bytes = 0, leaves_bytes = 0, always_geo_bytes = 0, always_sid_bytes = 0;
     rtk::BvhArgs bvh{};
     // optional per-kernel timing: event pairs around every sample / reduce launch of the last call
     bool timing = false;
@@ -130,38 +131,73 @@ int upload_bvh(rt_context* ctx, double bound) {
     ctx->bvh_ok = bvh.ok;
     ctx->bvh_origin_bound = bound;
     if (!bvh.ok) return RT_OK;
-    static_assert(sizeof(rtbvh::Node) == sizeof(rtk::BvhNode), "node layouts differ");
     static_assert(rtbvh::kLeafMax == rtk::kLeafBvh && rtbvh::kMaxDepth == rtk::kMaxDepthBvh, "BVH constants differ");
-    const size_t nn = bvh.nodes.size(), ns = bvh.slot_to_sphere.size();
-    std::vector<rtk::GeoRec> sgeo(ns ? ns : 1);
-    for (size_t q = 0; q < ns; q++) {
-        if (bvh.slot_to_sphere[q] == rtbvh::kSentinel) {  // never-hit padding slot
-            sgeo[q].cx = sgeo[q].cy = sgeo[q].cz = 0.0;
-            sgeo[q].r2 = -std::numeric_limits<double>::infinity();
-            continue;
+    const size_t nn = bvh.nodes.size();
+    const size_t na = bvh.n_always;
+    const size_t nl = (bvh.slot_to_sphere.size() - na) / rtk::kLeafBvh;
+    auto geo_of = [&](uint32_t k) {
+        rtk::GeoRec g;
+        if (k == rtbvh::kSentinel) {  // never-hit padding slot
+            g.cx = g.cy = g.cz = 0.0;
+            g.r2 = -std::numeric_limits<double>::infinity();
+            return g;
         }
-        const rt_sphere& sp = ctx->spheres[bvh.slot_to_sphere[q]];
+        const rt_sphere& sp = ctx->spheres[k];
         const double r = sp.radius > 0 ? sp.radius : 0.0;
-        sgeo[q].cx = sp.center[0];
-        sgeo[q].cy = sp.center[1];
-        sgeo[q].cz = sp.center[2];
-        sgeo[q].r2 = r * r;
+        g.cx = sp.center[0];
+        g.cy = sp.center[1];
+        g.cz = sp.center[2];
+        g.r2 = r * r;
+        return g;
+    };
+    std::vector<rtk::BvhNode> nodes(nn);
+    for (size_t i = 0; i < nn; i++) {
+        const rtbvh::Node& src = bvh.nodes[i];
+        rtk::BvhNode& d = nodes[i];
+        std::memset(&d, 0, sizeof d);
+        for (int a = 0; a < 3; a++) {
+            d.lo0[a] = src.lo0[a];
+            d.hi0[a] = src.hi0[a];
+            d.lo1[a] = src.lo1[a];
+            d.hi1[a] = src.hi1[a];
+        }
+        d.ref0 = src.ref0;
+        d.ref1 = src.ref1;
+    }
+    std::vector<rtk::BvhLeaf> leaves(nl ? nl : 1);
+    for (size_t l = 0; l < nl; l++)
+        for (int u = 0; u < rtk::kLeafBvh; u++) {
+            const uint32_t k = bvh.slot_to_sphere[na + l * rtk::kLeafBvh + u];
+            const rtk::GeoRec g = geo_of(k);
+            leaves[l].g[u] = rtk::LeafGeo{g.cx, g.cy, g.cz, g.r2};
+            leaves[l].sid[u] = k;
+        }
+    std::vector<rtk::GeoRec> ageo(na ? na : 1);
+    std::vector<uint32_t> asid(na ? na : 1, 0);
+    for (size_t q = 0; q < na; q++) {
+        ageo[q] = geo_of(bvh.slot_to_sphere[q]);
+        asid[q] = bvh.slot_to_sphere[q];
     }
     int rc = ensure_buffer((void**)&ctx->d_nodes, &ctx->nodes_bytes, nn * sizeof(rtk::BvhNode));
-    if (!rc) rc = ensure_buffer((void**)&ctx->d_slot_geo, &ctx->slot_geo_bytes, sgeo.size() * sizeof(rtk::GeoRec));
-    if (!rc) rc = ensure_buffer((void**)&ctx->d_slot_id, &ctx->slot_id_bytes, (ns ? ns : 1) * sizeof(uint32_t));
+    if (!rc) rc = ensure_buffer((void**)&ctx->d_leaves, &ctx->leaves_bytes, leaves.size() * sizeof(rtk::BvhLeaf));
+    if (!rc) rc = ensure_buffer((void**)&ctx->d_always_geo, &ctx->always_geo_bytes, ageo.size() * sizeof(rtk::GeoRec));
+    if (!rc) rc = ensure_buffer((void**)&ctx->d_always_sid, &ctx->always_sid_bytes, asid.size() * sizeof(uint32_t));
     if (rc) return rc;
-    HIP_CHECK(hipMemcpyAsync(ctx->d_nodes, bvh.nodes.data(), nn * sizeof(rtk::BvhNode), hipMemcpyHostToDevice, ctx->stream));
-    HIP_CHECK(hipMemcpyAsync(ctx->d_slot_geo, sgeo.data(), sgeo.size() * sizeof(rtk::GeoRec), hipMemcpyHostToDevice, ctx->stream));
-    if (ns)
-        HIP_CHECK(hipMemcpyAsync(ctx->d_slot_id, bvh.slot_to_sphere.data(), ns * sizeof(uint32_t), hipMemcpyHostToDevice, ctx->stream));
+    HIP_CHECK(hipMemcpyAsync(ctx->d_nodes, nodes.data(), nn * sizeof(rtk::BvhNode), hipMemcpyHostToDevice, ctx->stream));
+    HIP_CHECK(hipMemcpyAsync(ctx->d_leaves, leaves.data(), leaves.size() * sizeof(rtk::BvhLeaf), hipMemcpyHostToDevice,
+                             ctx->stream));
+    HIP_CHECK(hipMemcpyAsync(ctx->d_always_geo, ageo.data(), ageo.size() * sizeof(rtk::GeoRec), hipMemcpyHostToDevice,
+                             ctx->stream));
+    HIP_CHECK(hipMemcpyAsync(ctx->d_always_sid, asid.data(), asid.size() * sizeof(uint32_t), hipMemcpyHostToDevice,
+                             ctx->stream));
     HIP_CHECK(hipStreamSynchronize(ctx->stream));
     ctx->bvh.nodes = ctx->d_nodes;
-    ctx->bvh.slot_geo = ctx->d_slot_geo;
-    ctx->bvh.slot_id = ctx->d_slot_id;
+    ctx->bvh.leaves = ctx->d_leaves;
+    ctx->bvh.always_geo = ctx->d_always_geo;
+    ctx->bvh.always_sid = ctx->d_always_sid;
     ctx->bvh.n_nodes = (uint32_t)nn;
-    ctx->bvh.n_slots = (uint32_t)ns;
-    ctx->bvh.n_always = bvh.n_always;
+    ctx->bvh.n_leaves = (uint32_t)nl;
+    ctx->bvh.n_always = (uint32_t)na;
     return RT_OK;
 }
 
@@ -244,8 +280,9 @@ int rt_context_destroy(rt_context* ctx) {
     (void)hipFree(ctx->d_sums);
     (void)hipFree(ctx->d_queue);
     (void)hipFree(ctx->d_nodes);
-    (void)hipFree(ctx->d_slot_geo);
-    (void)hipFree(ctx->d_slot_id);
+    (void)hipFree(ctx->d_leaves);
+    (void)hipFree(ctx->d_always_geo);
+    (void)hipFree(ctx->d_always_sid);
     for (hipEvent_t e : ctx->events) (void)hipEventDestroy(e);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;

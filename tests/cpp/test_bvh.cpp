@@ -21,10 +21,10 @@ struct Box { double lo[3], hi[3]; };
 static void collect(const rtbvh::Bvh& b, int32_t ref, std::vector<uint32_t>& out, int depth, int& maxd) {
     if (depth > maxd) maxd = depth;
     if (ref < 0) {
-        const uint32_t code = (uint32_t)(~ref);
-        const uint32_t first = code >> 4, cnt = code & 15u;
-        CHECK(cnt == (uint32_t)rtbvh::kLeafMax, "leaf count %u", cnt);
-        for (uint32_t i = 0; i < cnt; i++) out.push_back(b.slot_to_sphere.at(first + i));
+        const uint32_t leaf = (uint32_t)(~ref);
+        const uint32_t first = b.n_always + leaf * rtbvh::kLeafMax;
+        CHECK(first + rtbvh::kLeafMax <= b.slot_to_sphere.size(), "leaf %u out of range", leaf);
+        for (uint32_t i = 0; i < (uint32_t)rtbvh::kLeafMax; i++) out.push_back(b.slot_to_sphere.at(first + i));
         return;
     }
     CHECK((size_t)ref < b.nodes.size(), "node ref %d", ref);
