@@ -18,7 +18,6 @@ sys.path.insert(0, os.path.join(ROOT, "raytracing-with-zig_amd"))
 import torch  # noqa: E402
 
 import rtzig  # noqa: E402
-from rtzig import lib as rlib  # noqa: E402
 
 ap = argparse.ArgumentParser()
 ap.add_argument("libs", nargs="+")
@@ -34,7 +33,16 @@ out = torch.empty((H, W, 3), dtype=torch.float64, device="cuda:0")
 runs = []
 for path in args.libs:
     L = C.CDLL(os.path.abspath(path))
-    rlib._declare(L)
+    vp = C.c_void_p
+    for name, res, argt in [("rt_context_create", C.c_int, [C.c_int, C.POINTER(vp)]),
+                            ("rt_context_set_scene", C.c_int, [vp, C.POINTER(rtzig.RtSphere), C.c_size_t]),
+                            ("rt_context_enable_timing", C.c_int, [vp, C.c_int]),
+                            ("rt_context_kernel_times", C.c_int, [vp, C.POINTER(C.c_double), C.POINTER(C.c_double)]),
+                            ("rt_render_rows_async", C.c_int, [vp, C.POINTER(rtzig.RtCamera), C.c_uint32, C.c_uint32,
+                                                               C.c_uint32, C.c_uint32, vp, vp, vp]),
+                            ("rt_last_error", C.c_char_p, [])]:
+        getattr(L, name).restype = res
+        getattr(L, name).argtypes = argt
     ctx = C.c_void_p()
     assert L.rt_context_create(0, C.byref(ctx)) == 0, L.rt_last_error()
     assert L.rt_context_set_scene(ctx, cam.scene.world, len(cam.scene.world)) == 0, L.rt_last_error()
