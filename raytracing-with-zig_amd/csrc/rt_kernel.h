@@ -43,7 +43,9 @@ struct KernelParams {
     uint32_t row0, row_step, n_rows, n_spheres;
     uint32_t n_pad;  // n_spheres rounded up to kPad (sentinel-padded)
     uint32_t s_begin, s_count;
-    uint32_t prof;  // 1: instrumented build, stats has 8 entries (see rt_context_enable_profile)
+    uint32_t prof;   // 1: instrumented build, stats has 8 entries (see rt_context_enable_profile)
+    uint32_t order;  // work-item order: 0 sample-major, 1 pixel-major (RTZIG_ORDER)
+    uint32_t pad2;
 };
 
 // BVH (rt_bvh.hpp).  Node = both child boxes (f32, padded outward) + child refs; ref >= 0 is a

@@ -312,7 +312,7 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
 
     // per-lane path state
     bool active = false;
-    uint64_t item = 0;
+    uint64_t item = 0, slot = 0;  // queue position; store position [s][pixel]
     Rng g;
     Ray r;
     v3 att = mk(1, 1, 1);
@@ -348,8 +348,15 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
                     active = true;
                     // items per launch < 2^32 (host-side chunking): 32-bit index math
                     const uint32_t it32 = (uint32_t)item;
-                    const uint32_t s_local = it32 / P;
-                    const uint32_t q = it32 - s_local * P;
+                    uint32_t s_local, q;
+                    if (p.order == 0) {  // sample-major: a wave takes 64 neighbouring pixels
+                        s_local = it32 / P;
+                        q = it32 - s_local * P;
+                    } else {  // pixel-major: a wave takes consecutive samples of one pixel
+                        q = it32 / p.s_count;
+                        s_local = it32 - q * p.s_count;
+                    }
+                    slot = (uint64_t)s_local * P + q;
                     const uint32_t row_local = q / W;
                     const uint32_t i = q - row_local * W;
                     const uint32_t j = p.row0 + row_local * p.row_step;
@@ -438,7 +445,7 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
                 }
             }
             if (done) {
-                double* dst = samples + 3 * item;
+                double* dst = samples + 3 * slot;
                 dst[0] = col.x;
                 dst[1] = col.y;
                 dst[2] = col.z;
