@@ -90,6 +90,8 @@ def main():
     ap.add_argument("--output", choices=["linear", "rgb8"], default="linear")
     ap.add_argument("--cpu-spp", type=int, default=4, help="spp of the bounded CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dist-backend", default="nccl",
+                    help="nccl (= RCCL over xGMI, the product) or gloo (rehearsal: several ranks on one GPU)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -97,10 +99,16 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if args.gpus != world and world > 1:
         log(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    # gloo rehearsal: ranks may share a device (local rank modulo the visible device count)
+    ndev = torch.cuda.device_count()
+    local_dev = local if args.dist_backend == "nccl" else local % max(1, ndev)
+    torch.cuda.set_device(local_dev)
+    dev = torch.device("cuda", local_dev)
     if world > 1:
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+        else:
+            dist.init_process_group("gloo", rank=rank, world_size=world)
 
     t_init = time.perf_counter()
     cam = rtzig.final_scene_camera(width=args.width, aspect_ratio=args.aspect, spp=args.spp)
@@ -108,7 +116,7 @@ def main():
     n_spheres = len(cam.scene.world)
     row0, step, n_rows = rdist.rank_rows(H, rank, world)
     R = rdist.rows_per_rank(H, world)
-    renderer = rtzig.DeviceRenderer(local)
+    renderer = rtzig.DeviceRenderer(local_dev)
     renderer.set_scene(cam.scene.world)
     renderer.enable_timing(True)
     if args.output == "linear":
@@ -127,7 +135,10 @@ def main():
             renderer.render_rows_async(cam.cam, out.data_ptr(), row0=row0, row_step=step,
                                        n_rows=n_rows, output=args.output, d_stats_ptr=stats_ptr,
                                        stream_ptr=stream.cuda_stream)
-        img = rdist.gather_image(out, H, rank, world)
+        if args.dist_backend == "gloo" and world > 1:
+            img = rdist.gather_image(out.cpu(), H, rank, world)  # gloo gathers host tensors
+        else:
+            img = rdist.gather_image(out, H, rank, world)
         if timed and n_rows:
             kernel_ms.append(renderer.kernel_times())
         return img
@@ -158,7 +169,8 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
 
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    t = torch.tensor([elapsed], dtype=torch.float64,
+                     device=dev if args.dist_backend == "nccl" else "cpu")
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed_max = float(t.item())
@@ -201,7 +213,9 @@ def main():
                     "seed 0xdeadbeef), main.zig camera preset",
             "config": {"workload": workload, "width": W, "height": H, "spp": spp, "depth": 50,
                        "spheres": n_spheres, "output": args.output,
-                       "parallelism": f"rows interleaved over {world} GPU(s), RCCL gather to rank 0"},
+                       "parallelism": f"rows interleaved over {world} GPU(s), "
+                           + ("RCCL gather to rank 0" if args.dist_backend == "nccl" else
+                              "gloo gather to rank 0 (rehearsal: ranks share devices)")},
             "roofline": {
                 "bound": "valu",
                 "kernel": renderer.kernel_name(),
