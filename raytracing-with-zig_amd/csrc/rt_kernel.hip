@@ -205,6 +205,10 @@ struct BvhWalker {
         if (__builtin_fabsf(dy) < 1e-30f) dy = __builtin_copysignf(1e-30f, dy);
         if (__builtin_fabsf(dz) < 1e-30f) dz = __builtin_copysignf(1e-30f, dz);
         const float ix = 1.0f / dx, iy = 1.0f / dy, iz = 1.0f / dz;
+        // slab planes as t = fma(bound, inv, -o*inv): one op per plane.  Error (position space,
+        // per axis) <= 2^-24 (3|bound| + 4|o|), inside the padding of rt_bvh.cpp; overflowed
+        // planes give inf/NaN, and NaN operands are dropped by fminf/fmaxf (permissive, so safe).
+        const float oix = ox * ix, oiy = oy * iy, oiz = oz * iz;
         float lower = (float)t_min;
         lower = lower - __builtin_fabsf(lower) * 0x1p-20f - 1e-30f;
         float upper = (float)closest;
@@ -222,16 +226,16 @@ struct BvhWalker {
                 const BvhNode nd = nodes[cur];
                 float n0, f0, n1, f1;
                 {
-                    const float ax0 = (nd.lo0[0] - ox) * ix, bx0 = (nd.hi0[0] - ox) * ix;
-                    const float ay0 = (nd.lo0[1] - oy) * iy, by0 = (nd.hi0[1] - oy) * iy;
-                    const float az0 = (nd.lo0[2] - oz) * iz, bz0 = (nd.hi0[2] - oz) * iz;
+                    const float ax0 = __builtin_fmaf(nd.lo0[0], ix, -oix), bx0 = __builtin_fmaf(nd.hi0[0], ix, -oix);
+                    const float ay0 = __builtin_fmaf(nd.lo0[1], iy, -oiy), by0 = __builtin_fmaf(nd.hi0[1], iy, -oiy);
+                    const float az0 = __builtin_fmaf(nd.lo0[2], iz, -oiz), bz0 = __builtin_fmaf(nd.hi0[2], iz, -oiz);
                     n0 = __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(ax0, bx0), __builtin_fminf(ay0, by0)),
                                          __builtin_fmaxf(__builtin_fminf(az0, bz0), lower));
                     f0 = __builtin_fminf(__builtin_fminf(__builtin_fmaxf(ax0, bx0), __builtin_fmaxf(ay0, by0)),
                                          __builtin_fminf(__builtin_fmaxf(az0, bz0), upper));
-                    const float ax1 = (nd.lo1[0] - ox) * ix, bx1 = (nd.hi1[0] - ox) * ix;
-                    const float ay1 = (nd.lo1[1] - oy) * iy, by1 = (nd.hi1[1] - oy) * iy;
-                    const float az1 = (nd.lo1[2] - oz) * iz, bz1 = (nd.hi1[2] - oz) * iz;
+                    const float ax1 = __builtin_fmaf(nd.lo1[0], ix, -oix), bx1 = __builtin_fmaf(nd.hi1[0], ix, -oix);
+                    const float ay1 = __builtin_fmaf(nd.lo1[1], iy, -oiy), by1 = __builtin_fmaf(nd.hi1[1], iy, -oiy);
+                    const float az1 = __builtin_fmaf(nd.lo1[2], iz, -oiz), bz1 = __builtin_fmaf(nd.hi1[2], iz, -oiz);
                     n1 = __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(ax1, bx1), __builtin_fminf(ay1, by1)),
                                          __builtin_fmaxf(__builtin_fminf(az1, bz1), lower));
                     f1 = __builtin_fminf(__builtin_fminf(__builtin_fmaxf(ax1, bx1), __builtin_fmaxf(ay1, by1)),
