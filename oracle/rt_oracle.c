@@ -553,3 +553,48 @@ EXPORT void oracle_refract(const double* v, const double* n, double eta, double*
     const v3 r = refract(V(v[0], v[1], v[2]), V(n[0], n[1], n[2]), eta);
     out[0] = r.x; out[1] = r.y; out[2] = r.z;
 }
+
+/* ------------------------------------------------------------------------------------------------
+ * BASELINE config 1: "chapter5 single-sphere, 400x225, 1 spp" — the book's chapter 4/5 renderer
+ * that produced test-files/chapter4.ppm / chapter5.ppm (earlier book-chapter code, no longer in
+ * src/; restated from the fixtures' own pixels): focal length 1, viewport height 2, camera at the
+ * origin, one centered ray per pixel (no RNG), sky lerp (camera.zig:171-177); chapter 5 adds a
+ * red sphere (0,0,-1) r 0.5 hit when disc >= 0 (sphere.zig:27-33 without the root test); colors
+ * quantised as trunc(255.999 * c) with no gamma.  Byte-exact vs both fixtures (tests/test_oracle.py).
+ * ---------------------------------------------------------------------------------------------- */
+EXPORT int oracle_render_book(int chapter, uint32_t width, double ratio, uint8_t* rgb, uint32_t* height_out) {
+    size_t h = (size_t)((double)width / ratio);
+    if (h < 1) h = 1;
+    const double W = (double)width, H = (double)h;
+    const double vp_h = 2.0, vp_w = vp_h * (W / H);
+    const v3 center = V(0, 0, 0);
+    const v3 vu = V(vp_w, 0, 0), vv = V(0, -vp_h, 0);
+    const v3 du = divs(vu, W), dv = divs(vv, H);
+    const v3 ul = sub(sub(sub(center, V(0, 0, 1.0)), divs(vu, 2)), divs(vv, 2));
+    const v3 p00 = add(ul, muls(add(du, dv), 0.5));
+    for (size_t j = 0; j < h; j++) {
+        for (uint32_t i = 0; i < width; i++) {
+            const v3 pc = add(add(p00, muls(du, (double)i)), muls(dv, (double)j));
+            const v3 d = sub(pc, center);
+            v3 col;
+            int hit = 0;
+            if (chapter == 5) {
+                const v3 oc = sub(V(0, 0, -1), center);
+                const double a = len_sq(d), hh = dot(d, oc), c = len_sq(oc) - 0.5 * 0.5;
+                hit = hh * hh - a * c >= 0;
+            }
+            if (hit) {
+                col = V(1, 0, 0);
+            } else {
+                const double a = 0.5 * (unit(d).y + 1.0);
+                col = add(muls(V(1, 1, 1), 1.0 - a), muls(V(0.5, 0.7, 1), a));
+            }
+            uint8_t* o = rgb + 3 * (j * width + i);
+            o[0] = (uint8_t)(int)(255.999 * col.x);
+            o[1] = (uint8_t)(int)(255.999 * col.y);
+            o[2] = (uint8_t)(int)(255.999 * col.z);
+        }
+    }
+    if (height_out) *height_out = (uint32_t)h;
+    return 0;
+}

@@ -36,6 +36,7 @@ class Oracle:
         L.oracle_world_hit.restype = C.c_long
         L.oracle_random_doubles.argtypes = [C.c_uint64, C.c_size_t, dp]
         L.oracle_random_u64.argtypes = [C.c_uint64, C.c_size_t, P(C.c_uint64)]
+        L.oracle_render_book.argtypes = [C.c_int, C.c_uint32, C.c_double, P(C.c_uint8), P(C.c_uint32)]
         L.oracle_reflect.argtypes = [dp, dp, dp]
         L.oracle_refract.argtypes = [dp, dp, C.c_double, dp]
         self.L = L
@@ -93,6 +94,15 @@ class Oracle:
         buf = (C.c_uint8 * size)()
         self.L.oracle_ppm_p6(rgb.ctypes.data_as(P(C.c_uint8)), w, h, buf, size)
         return bytes(buf)
+
+    def render_book(self, chapter, width=400, ratio=16.0 / 9.0):
+        """BASELINE config 1 (book chapter 4/5 renderer): (H, W, 3) uint8."""
+        h = max(1, int(width / ratio))
+        rgb = np.zeros((h, width, 3), np.uint8)
+        hh = C.c_uint32()
+        self.L.oracle_render_book(chapter, width, ratio, rgb.ctypes.data_as(P(C.c_uint8)), C.byref(hh))
+        assert hh.value == h
+        return rgb
 
     # ---- KAT helpers ----------------------------------------------------------------------------
     def sample_key(self, seed, pixel, sample):

@@ -154,3 +154,14 @@ def test_oracle_b_statistically_matches_golden(oracle, golden_dir):
     assert np.abs(rgb.mean(axis=(0, 1)) - gold.mean(axis=(0, 1))).max() <= 1.0
     box = lambda x: x[:224].reshape(28, 8, 50, 8, 3).mean(axis=(1, 3))
     assert np.sqrt(((box(rgb) - box(gold)) ** 2).mean()) <= 2.0
+
+
+@pytest.mark.parametrize("chapter", [4, 5])
+def test_config1_book_chapter_byte_exact(oracle, golden_dir, chapter):
+    """BASELINE config 1 (chapter5 single sphere, 400x225, 1 spp, CPU plumbing + PPM diff):
+    the book renderer restated in the oracle + the P6 writer reproduce test-files/chapter{4,5}.ppm."""
+    rgb = oracle.render_book(chapter)
+    data = oracle.ppm_p6(rgb, 400, 225)
+    assert data == open(os.path.join(golden_dir, f"chapter{chapter}.ppm"), "rb").read()
+    import rtzig
+    assert rtzig.encode_p6(rgb, 400, 225) == data  # the product's P6 writer too
