@@ -73,6 +73,10 @@ struct Rng {
 
     // DefaultPrng.init(key): Xoshiro256.seed via SplitMix64 (zig std/Random/Xoshiro256.zig)
     __device__ __forceinline__ void seed(uint64_t key) {
+#ifdef RTZIG_ABLATE_SEED  // timing ablation only: no SplitMix64 seeding
+        s0 = key; s1 = key ^ 0x1234567887654321ULL; s2 = ~key; s3 = key ^ 0x0f0f0f0ff0f0f0f0ULL;
+        return;
+#endif
         uint64_t sm = key;
         s0 = splitmix_next(sm);
         s1 = splitmix_next(sm);
@@ -121,6 +125,14 @@ __device__ __forceinline__ uint64_t sample_key(uint64_t seed_mix, uint64_t pixel
 
 // Vec.randomUnitVec (vec.zig:71-80): rejection in the cube, then TRUE division by the length.
 __device__ __forceinline__ v3 random_unit_vec(Rng& g) {
+#ifdef RTZIG_ABLATE_RUV  // timing ablation only (wrong distribution): one candidate, no loop
+    {
+        const double x = g.range(-1, 1), y = g.range(-1, 1), z = g.range(-1, 1);
+        const double ls = (x * x + y * y) + z * z;
+        const double l = __builtin_sqrt(ls > 1e-160 ? ls : 1.0);
+        return v3{x / l, y / l, z / l};
+    }
+#endif
     for (;;) {
         const double x = g.range(-1, 1);
         const double y = g.range(-1, 1);

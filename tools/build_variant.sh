@@ -6,6 +6,18 @@ ROOT=$(cd "$(dirname "$0")/.." && pwd)
 REV=$1; NAME=$2
 mkdir -p "$ROOT/ab"
 if [ "$REV" = "WORKTREE" ]; then
+  # EXTRA: extra compiler flags for ablation builds (e.g. -DRTZIG_ABLATE_RUV), built out of tree
+  if [ -n "$EXTRA" ]; then
+    B=/tmp/rtab_$NAME; rm -rf "$B"; mkdir -p "$B"
+    C="$ROOT/raytracing-with-zig_amd/csrc"
+    F="-O3 -std=c++17 -fPIC -ffp-contract=off -Wno-unused-function $EXTRA"
+    /opt/rocm/bin/hipcc $F -x hip --offload-arch=gfx950 -fno-gpu-rdc -c "$C/rt_kernel.hip" -o "$B/k.o"
+    /opt/rocm/bin/hipcc $F -x hip --offload-arch=gfx950 -fno-gpu-rdc -c "$C/rt_runtime.cpp" -o "$B/r.o"
+    /opt/rocm/bin/hipcc $F -x c++ -c "$C/rt_host.cpp" -o "$B/h.o"
+    /opt/rocm/bin/hipcc $F -x c++ -c "$C/rt_bvh.cpp" -o "$B/b.o"
+    /opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o "$ROOT/ab/$NAME.so" "$B"/*.o
+    echo "ab/$NAME.so"; exit 0
+  fi
   make -s -C "$ROOT/raytracing-with-zig_amd/csrc" >/dev/null
   cp "$ROOT/raytracing-with-zig_amd/librtzig.so" "$ROOT/ab/$NAME.so"
 else
