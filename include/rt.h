@@ -123,10 +123,11 @@ const char* rt_kernel_name(rt_context* ctx);
  * summed durations (ms) of the most recent rt_render_rows_async call. */
 int rt_context_enable_timing(rt_context* ctx, int enable);
 int rt_context_kernel_times(rt_context* ctx, double* sample_ms, double* reduce_ms);
-/* Instrumented kernels (diagnostics): when enabled, `d_stats` of rt_render_rows_async must hold 8
+/* Instrumented kernels (diagnostics): when enabled, `d_stats` of rt_render_rows_async must hold 16
  * uint64: {rays, samples, sphere tests executed, BVH node visits, wave-cycles in queue refill,
- * wave-cycles in the closest-hit walk, wave-cycles in shading, 0}.  The first four are exact,
- * deterministic counts; the cycles are s_memtime diagnostics. */
+ * wave-cycles in the closest-hit walk, wave-cycles in shading, wave-iterations of the BVH inner
+ * (internal-node) loop, wave-iterations of BVH leaf rounds, 0...}.  Counts 0-3 are exact and
+ * deterministic; the cycles and wave-iteration counts are diagnostics. */
 int rt_context_enable_profile(rt_context* ctx, int enable);
 
 /* ---- host mirror of the reference's Scene / CameraBuilder / Color / PPM ---------------------- */

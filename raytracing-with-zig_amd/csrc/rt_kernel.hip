@@ -121,12 +121,21 @@ template <bool kOn>
 struct Prof {
     __device__ __forceinline__ void tests(uint32_t) {}
     __device__ __forceinline__ void visit() {}
+    __device__ __forceinline__ void inner_iter() {}
+    __device__ __forceinline__ void leaf_iter() {}
 };
 template <>
 struct Prof<true> {
     uint64_t n_tests = 0, n_visits = 0;
+    uint64_t w_inner = 0, w_leaf = 0;  // wave-level iterations (counted by the first active lane)
     __device__ __forceinline__ void tests(uint32_t n) { n_tests += n; }
     __device__ __forceinline__ void visit() { ++n_visits; }
+    __device__ __forceinline__ static bool leader() {
+        const uint64_t m = __ballot(1);
+        return (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u)) == 0;
+    }
+    __device__ __forceinline__ void inner_iter() { w_inner += leader() ? 1 : 0; }
+    __device__ __forceinline__ void leaf_iter() { w_leaf += leader() ? 1 : 0; }
 };
 
 // ------------------------------------------------------------------------------------------------
@@ -223,6 +232,7 @@ struct BvhWalker {
         while (cur != kDone) {
             while (cur >= 0) {
                 pr.visit();
+                pr.inner_iter();
                 const BvhNode nd = nodes[cur];
                 float n0, f0, n1, f1;
                 {
@@ -261,6 +271,7 @@ struct BvhWalker {
                 }
             }
             if (cur != kDone) {
+                pr.leaf_iter();
                 // leaf: exactly kLeafBvh slots (sentinel-padded); the four discriminant chains
                 // are independent, the candidate updates then run in slot order
                 const BvhLeaf* lf = leaves + (uint32_t)(~cur);
@@ -491,9 +502,16 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
                 nt += __shfl_xor(nt, off, 64);
                 nv += __shfl_xor(nv, off, 64);
             }
+            uint64_t wi = pr.w_inner, wl = pr.w_leaf;
+            for (int off = 32; off > 0; off >>= 1) {
+                wi += __shfl_xor(wi, off, 64);
+                wl += __shfl_xor(wl, off, 64);
+            }
             if (lane == 0) {
                 atomicAdd(&stats[2], (unsigned long long)nt);
                 atomicAdd(&stats[3], (unsigned long long)nv);
+                atomicAdd(&stats[7], (unsigned long long)wi);
+                atomicAdd(&stats[8], (unsigned long long)wl);
                 atomicAdd(&stats[4], (unsigned long long)cyc_refill);
                 atomicAdd(&stats[5], (unsigned long long)cyc_walk);
                 atomicAdd(&stats[6], (unsigned long long)cyc_shade);

@@ -29,7 +29,7 @@ r = rtzig.DeviceRenderer(0)
 r.set_scene(cam.scene.world)
 r.enable_timing(True)
 out = torch.empty((H, W, 3), dtype=torch.float64, device="cuda:0")
-stats = torch.zeros(8, dtype=torch.int64, device="cuda:0")
+stats = torch.zeros(16, dtype=torch.int64, device="cuda:0")
 res = {"config": f"{W}x{H} {args.spp}spp, {len(cam.scene.world)} spheres", "variants": {}}
 for v in args.variants.split():
     os.environ["RTZIG_KERNEL"] = v
@@ -48,6 +48,9 @@ for v in args.variants.split():
         "kernel": r.kernel_name(), "sample_kernel_ms": round(plain_ms, 3), "instrumented_ms": round(prof_ms, 3),
         "rays": s[0], "samples": s[1], "rays_per_sample": round(s[0] / s[1], 4),
         "sphere_tests_per_ray": round(s[2] / s[0], 3), "node_visits_per_ray": round(s[3] / s[0], 3),
+        "wave_inner_iters_per_wave_iter": round(s[7] / max(1, s[0] / 64), 3),
+        "wave_leaf_rounds_per_wave_iter": round(s[8] / max(1, s[0] / 64), 3),
+        "lane_util_inner": round(s[3] / max(1, s[7] * 64), 4),
         "cycle_split": {"refill": round(s[4] / cyc, 4), "walk": round(s[5] / cyc, 4), "shade": round(s[6] / cyc, 4)},
         "raw": s,
     }
