@@ -160,7 +160,6 @@ struct LinearWalker {
 // same f64 quadratic as the linear walk; the candidate root of sphere k is
 //   t_k = root1 if t_min < root1, else root2 if t_min < root2   (sphere.zig:38-41),
 // and it wins iff t_k < closest, or t_k == closest and k is lower (the linear scan's first-wins).
-template <bool kSpec>
 struct BvhWalker {
     const BvhNode* __restrict__ nodes;
     const BvhLeaf* __restrict__ leaves;
@@ -226,120 +225,79 @@ struct BvhWalker {
 
         int sp = 0;
         int32_t cur = 0;  // root
+        // while-while (Aila & Laine 2009): every lane advances through internal nodes until it
+        // holds a leaf (or is done); then the lanes with a leaf test its spheres together, so the
+        // f64 leaf work runs with most lanes active instead of whenever any one lane hits a leaf.
         constexpr int32_t kDone = INT32_MIN;
-
-        // one internal-node step: test both child boxes, descend near-first, push the far child
-        auto internal_step = [&]() {
-            pr.visit();
-            const BvhNode nd = nodes[cur];
-            float n0, f0, n1, f1;
-            {
-                const float ax0 = __builtin_fmaf(nd.lo0[0], ix, -oix), bx0 = __builtin_fmaf(nd.hi0[0], ix, -oix);
-                const float ay0 = __builtin_fmaf(nd.lo0[1], iy, -oiy), by0 = __builtin_fmaf(nd.hi0[1], iy, -oiy);
-                const float az0 = __builtin_fmaf(nd.lo0[2], iz, -oiz), bz0 = __builtin_fmaf(nd.hi0[2], iz, -oiz);
-                n0 = __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(ax0, bx0), __builtin_fminf(ay0, by0)),
-                                     __builtin_fmaxf(__builtin_fminf(az0, bz0), lower));
-                f0 = __builtin_fminf(__builtin_fminf(__builtin_fmaxf(ax0, bx0), __builtin_fmaxf(ay0, by0)),
-                                     __builtin_fminf(__builtin_fmaxf(az0, bz0), upper));
-                const float ax1 = __builtin_fmaf(nd.lo1[0], ix, -oix), bx1 = __builtin_fmaf(nd.hi1[0], ix, -oix);
-                const float ay1 = __builtin_fmaf(nd.lo1[1], iy, -oiy), by1 = __builtin_fmaf(nd.hi1[1], iy, -oiy);
-                const float az1 = __builtin_fmaf(nd.lo1[2], iz, -oiz), bz1 = __builtin_fmaf(nd.hi1[2], iz, -oiz);
-                n1 = __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(ax1, bx1), __builtin_fminf(ay1, by1)),
-                                     __builtin_fmaxf(__builtin_fminf(az1, bz1), lower));
-                f1 = __builtin_fminf(__builtin_fminf(__builtin_fmaxf(ax1, bx1), __builtin_fmaxf(ay1, by1)),
-                                     __builtin_fminf(__builtin_fmaxf(az1, bz1), upper));
+        while (cur != kDone) {
+            while (cur >= 0) {
+                pr.visit();
+                pr.inner_iter();
+                const BvhNode nd = nodes[cur];
+                float n0, f0, n1, f1;
+                {
+                    const float ax0 = __builtin_fmaf(nd.lo0[0], ix, -oix), bx0 = __builtin_fmaf(nd.hi0[0], ix, -oix);
+                    const float ay0 = __builtin_fmaf(nd.lo0[1], iy, -oiy), by0 = __builtin_fmaf(nd.hi0[1], iy, -oiy);
+                    const float az0 = __builtin_fmaf(nd.lo0[2], iz, -oiz), bz0 = __builtin_fmaf(nd.hi0[2], iz, -oiz);
+                    n0 = __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(ax0, bx0), __builtin_fminf(ay0, by0)),
+                                         __builtin_fmaxf(__builtin_fminf(az0, bz0), lower));
+                    f0 = __builtin_fminf(__builtin_fminf(__builtin_fmaxf(ax0, bx0), __builtin_fmaxf(ay0, by0)),
+                                         __builtin_fminf(__builtin_fmaxf(az0, bz0), upper));
+                    const float ax1 = __builtin_fmaf(nd.lo1[0], ix, -oix), bx1 = __builtin_fmaf(nd.hi1[0], ix, -oix);
+                    const float ay1 = __builtin_fmaf(nd.lo1[1], iy, -oiy), by1 = __builtin_fmaf(nd.hi1[1], iy, -oiy);
+                    const float az1 = __builtin_fmaf(nd.lo1[2], iz, -oiz), bz1 = __builtin_fmaf(nd.hi1[2], iz, -oiz);
+                    n1 = __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(ax1, bx1), __builtin_fminf(ay1, by1)),
+                                         __builtin_fmaxf(__builtin_fminf(az1, bz1), lower));
+                    f1 = __builtin_fminf(__builtin_fminf(__builtin_fmaxf(ax1, bx1), __builtin_fmaxf(ay1, by1)),
+                                         __builtin_fminf(__builtin_fmaxf(az1, bz1), upper));
+                }
+                const bool h0 = n0 <= f0;
+                const bool h1 = n1 <= f1;
+                // both hit: descend into the nearer child and push the farther one (the store
+                // always happens; it only counts when sp advances); one hit: descend; none: pop
+                const bool first0 = n0 <= n1;
+                const int32_t near_ref = first0 ? nd.ref0 : nd.ref1;
+                const int32_t far_ref = first0 ? nd.ref1 : nd.ref0;
+                stack[sp * kBlockBvh] = far_ref;
+                const bool both = h0 && h1;
+                sp += both ? 1 : 0;
+                if (h0 || h1) {
+                    cur = both ? near_ref : (h0 ? nd.ref0 : nd.ref1);
+                } else if (sp == 0) {
+                    cur = kDone;
+                } else {
+                    --sp;
+                    cur = stack[sp * kBlockBvh];
+                }
             }
-            const bool h0 = n0 <= f0;
-            const bool h1 = n1 <= f1;
-            // both hit: descend into the nearer child and push the farther one (the store
-            // always happens; it only counts when sp advances); one hit: descend; none: pop
-            const bool first0 = n0 <= n1;
-            const int32_t near_ref = first0 ? nd.ref0 : nd.ref1;
-            const int32_t far_ref = first0 ? nd.ref1 : nd.ref0;
-            stack[sp * kBlockBvh] = far_ref;
-            const bool both = h0 && h1;
-            sp += both ? 1 : 0;
-            if (h0 || h1) {
-                cur = both ? near_ref : (h0 ? nd.ref0 : nd.ref1);
-            } else if (sp == 0) {
-                cur = kDone;
-            } else {
-                --sp;
-                cur = stack[sp * kBlockBvh];
-            }
-        };
-        // leaf: exactly kLeafBvh slots (sentinel-padded); the four discriminant chains are
-        // independent, the candidate updates then run in slot order
-        auto leaf_test = [&](int32_t ref) {
-            const BvhLeaf* lf = leaves + (uint32_t)(~ref);
-            double h[kLeafBvh], disc[kLeafBvh];
+            if (cur != kDone) {
+                pr.leaf_iter();
+                // leaf: exactly kLeafBvh slots (sentinel-padded); the four discriminant chains
+                // are independent, the candidate updates then run in slot order
+                const BvhLeaf* lf = leaves + (uint32_t)(~cur);
+                double h[kLeafBvh], disc[kLeafBvh];
 #pragma unroll
-            for (int u = 0; u < kLeafBvh; ++u) {
-                const LeafGeo g = lf->g[u];
-                const double ocx = g.cx - r.orig.x;
-                const double ocy = g.cy - r.orig.y;
-                const double ocz = g.cz - r.orig.z;
-                h[u] = (r.dir.x * ocx + r.dir.y * ocy) + r.dir.z * ocz;
-                const double c = ((ocx * ocx + ocy * ocy) + ocz * ocz) - g.r2;
-                disc[u] = h[u] * h[u] - a * c;
-            }
+                for (int u = 0; u < kLeafBvh; ++u) {
+                    const LeafGeo s = lf->g[u];
+                    const double ocx = s.cx - r.orig.x;
+                    const double ocy = s.cy - r.orig.y;
+                    const double ocz = s.cz - r.orig.z;
+                    h[u] = (r.dir.x * ocx + r.dir.y * ocy) + r.dir.z * ocz;
+                    const double c = ((ocx * ocx + ocy * ocy) + ocz * ocz) - s.r2;
+                    disc[u] = h[u] * h[u] - a * c;
+                }
 #pragma unroll
-            for (int u = 0; u < kLeafBvh; ++u) {
-                if (disc[u] >= 0) candidate(lf->sid[u], h[u], disc[u], a, t_min, closest, best, found);
-            }
-            pr.tests(kLeafBvh);
-            upper = (float)closest;
-            upper = upper + __builtin_fabsf(upper) * 0x1p-20f;
-        };
-        auto pop = [&]() {
-            if (sp == 0) {
-                cur = kDone;
-            } else {
-                --sp;
-                cur = stack[sp * kBlockBvh];
-            }
-        };
-
-        if constexpr (!kSpec) {
-            // while-while (Aila & Laine 2009): every lane advances through internal nodes until it
-            // holds a leaf (or is done); then the lanes with a leaf test its spheres together, so
-            // the f64 leaf work runs with most lanes active
-            while (cur != kDone) {
-                while (cur >= 0) {
-                    pr.inner_iter();
-                    internal_step();
+                for (int u = 0; u < kLeafBvh; ++u) {
+                    if (disc[u] >= 0) candidate(lf->sid[u], h[u], disc[u], a, t_min, closest, best, found);
                 }
-                if (cur != kDone) {
-                    pr.leaf_iter();
-                    leaf_test(cur);
-                    pop();
-                }
-            }
-        } else {
-            // speculative while-while: a lane that reaches a leaf postpones it and keeps descending
-            // until EVERY lane holds a leaf (or is done), so each leaf round runs with more lanes.
-            // The culling bound is only ever looser than the true closest: exactness unaffected.
-            constexpr int32_t kNone = INT32_MAX;
-            int32_t post = kNone;
-            while (true) {
-                while (true) {
-                    const bool move = cur >= 0 || (cur != kDone && post == kNone);
-                    if (!__any(move)) break;
-                    if (move) {
-                        pr.inner_iter();
-                        if (cur >= 0) {
-                            internal_step();
-                        } else {
-                            post = cur;
-                            pop();
-                        }
-                    }
-                }
-                if (!__any(post != kNone)) break;
-                if (post != kNone) {
-                    pr.leaf_iter();
-                    leaf_test(post);
-                    post = kNone;
+                pr.tests(kLeafBvh);
+                upper = (float)closest;
+                upper = upper + __builtin_fabsf(upper) * 0x1p-20f;
+                if (sp == 0) {
+                    cur = kDone;
+                } else {
+                    --sp;
+                    cur = stack[sp * kBlockBvh];
                 }
             }
         }
@@ -579,7 +537,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kWaves))
 
 // BVH-walk kernel: nodes + slot geometry + slot ids staged in LDS (kLdsScene) or read from global
 // memory; the per-lane traversal stack always lives in LDS.
-template <bool kLdsScene, bool kProf, bool kSpec>
+template <bool kLdsScene, bool kProf>
 __global__ __launch_bounds__(kBlockBvh) void sample_kernel_bvh(KernelParams p, BvhArgs b,
                                                                const GeoRec* __restrict__ geo_g,
                                                                const MatRec* __restrict__ mat_g,
@@ -600,8 +558,8 @@ __global__ __launch_bounds__(kBlockBvh) void sample_kernel_bvh(KernelParams p, B
         nodes = ln;
         leaves = ll;
     }
-    path_loop<kProf>(p, BvhWalker<kSpec>{nodes, leaves, b.always_geo, b.always_sid, b.n_always, stack + threadIdx.x},
-                     geo_g, mat_g, samples, queue, stats);
+    path_loop<kProf>(p, BvhWalker{nodes, leaves, b.always_geo, b.always_sid, b.n_always, stack + threadIdx.x}, geo_g,
+                     mat_g, samples, queue, stats);
 }
 
 template <int kOut>
@@ -757,21 +715,10 @@ extern "C" hipError_t rtk_launch_samples_bvh(const rtk::KernelParams* p, const r
         hipLaunchKernelGGL(kernel, dim3(blocks), dim3(kBlockBvh), shmem, stream, *p, *b, geo, mat, samples, qu, st);
         return hipGetLastError();
     };
-    const char* env = std::getenv("RTZIG_KERNEL");
-    const bool spec = env && std::strcmp(env, "bvh_spec") == 0;
-#define RTK_BVH(L, P, S, NM)                                   \
-    if (lds_scene == L && (p->prof != 0) == P && spec == S)    \
-        return launch(sample_kernel_bvh<L, P, S>, NM);
-    RTK_BVH(true, false, false, "bvh_lds")
-    RTK_BVH(false, false, false, "bvh_global")
-    RTK_BVH(true, true, false, "bvh_lds(prof)")
-    RTK_BVH(false, true, false, "bvh_global(prof)")
-    RTK_BVH(true, false, true, "bvh_spec_lds")
-    RTK_BVH(false, false, true, "bvh_spec_global")
-    RTK_BVH(true, true, true, "bvh_spec_lds(prof)")
-    RTK_BVH(false, true, true, "bvh_spec_global(prof)")
-#undef RTK_BVH
-    return hipErrorInvalidValue;
+    if (p->prof)
+        return lds_scene ? launch(sample_kernel_bvh<true, true>, "bvh_lds(prof)")
+                         : launch(sample_kernel_bvh<false, true>, "bvh_global(prof)");
+    return lds_scene ? launch(sample_kernel_bvh<true, false>, "bvh_lds") : launch(sample_kernel_bvh<false, false>, "bvh_global");
 }
 
 extern "C" hipError_t rtk_launch_reduce(const rtk::ReduceParams* p, const double* samples, double* sums,

@@ -215,7 +215,7 @@ def test_c_harness_end_to_end(tmp_path):
     assert open(out, "rb").read() == rtzig.encode_p6(rgb, 400, 225)
 
 
-@pytest.mark.parametrize("variant", ["bvh", "bvh_spec", "smem_u4", "smem_u1", "lds_u2", "lds_u4"])
+@pytest.mark.parametrize("variant", ["bvh", "smem_u4", "smem_u1", "lds_u2", "lds_u4"])
 def test_walk_variants_bit_exact(oracle, variant, monkeypatch):
     """Every closest-hit walk (BVH and the linear list walks) gives oracle B's bits: golden config
     + the degenerate-materials scene."""
@@ -230,12 +230,11 @@ def test_walk_variants_bit_exact(oracle, variant, monkeypatch):
     assert np.array_equal(out, ref)
 
 
-@pytest.mark.parametrize("walk", ["bvh", "bvh_spec"])
 @pytest.mark.parametrize("seed", [1, 2, 3])
-def test_bvh_random_scenes_bit_exact(oracle, seed, walk, monkeypatch):
+def test_bvh_random_scenes_bit_exact(oracle, seed, monkeypatch):
     """BVH culling stress: random sphere soups (overlapping, duplicated, tiny and huge spheres,
     negative radii) from random camera positions; the BVH walk must return the linear scan's bits."""
-    monkeypatch.setenv("RTZIG_KERNEL", walk)
+    monkeypatch.setenv("RTZIG_KERNEL", "bvh")
     rng = np.random.default_rng(seed)
     n = int(rng.integers(2, 300))
     arr = (RtSphere * (n + 2))()
