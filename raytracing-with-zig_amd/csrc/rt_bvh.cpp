@@ -11,6 +11,9 @@
 #include "rt_bvh.hpp"
 
 #include <algorithm>
+#include <cstdlib>
+#include <utility>
+#include <vector>
 #include <cmath>
 #include <limits>
 #include <numeric>
@@ -193,6 +196,33 @@ Bvh build(const rt_sphere* spheres, size_t n, double origin_bound) {
         }
         p.sphere = (uint32_t)k;
         B.prims.push_back(p);
+    }
+    // Huge spheres (a ground plane of radius 1000) go to the always-list: their box spans the
+    // scene, so in the tree they cost a leaf round for most rays and inflate every ancestor box;
+    // tested up front in lockstep they cost one sphere test per ray and hand the traversal a
+    // tight `closest` to cull against.  Criterion: box surface area >= kAlwaysArea x the area of
+    // the box of all boundable spheres, at most kMaxBig of them (largest first).
+    if (B.prims.size() > (size_t)kLeafMax) {
+        double lo[3], hi[3];
+        B.bounds(0, B.prims.size(), lo, hi);
+        const double total = Builder::area(lo, hi);
+        double frac = kAlwaysArea;
+        if (const char* e = std::getenv("RTZIG_BVH_ALWAYS_AREA")) frac = std::atof(e);  // A/B knob
+        std::vector<std::pair<double, size_t>> big;
+        for (size_t i = 0; i < B.prims.size(); i++) {
+            const double a = Builder::area(B.prims[i].lo, B.prims[i].hi);
+            if (frac > 0 && a >= frac * total) big.push_back({-a, i});
+        }
+        std::sort(big.begin(), big.end());
+        if (big.size() > (size_t)kMaxBig) big.resize(kMaxBig);
+        std::vector<char> drop(B.prims.size(), 0);
+        for (auto& bg : big) drop[bg.second] = 1;
+        std::vector<Prim> keep;
+        for (size_t i = 0; i < B.prims.size(); i++) {
+            if (drop[i]) always.push_back(B.prims[i].sphere);
+            else keep.push_back(B.prims[i]);
+        }
+        B.prims.swap(keep);
     }
     B.slot_base = (uint32_t)always.size();
     const size_t m = B.prims.size();

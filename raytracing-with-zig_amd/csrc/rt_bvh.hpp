@@ -17,13 +17,18 @@
 
 namespace rtbvh {
 
-constexpr int kLeafMax = 4;   // spheres per leaf
+#ifndef RTZIG_LEAF
+#define RTZIG_LEAF 2
+#endif
+constexpr int kLeafMax = RTZIG_LEAF;   // spheres per leaf (build knob; A/B on config 4: 2 < 4 < 3 ms, 1 and 8 clearly slower)
 constexpr int kMaxDepth = 16; // tree depth bound == per-lane stack size in the kernel
+constexpr double kAlwaysArea = 0.25;  // box-area fraction above which a sphere is tested always
+constexpr int kMaxBig = 4;           // at most this many such spheres
 constexpr uint32_t kSentinel = 0xffffffffu;  // slot_to_sphere value of a padding slot
 
 // Internal node: the boxes of both children (f32, padded outward) and their refs.
 // ref >= 0: internal node index; ref < 0: leaf index ~ref.  Leaf L holds slots
-// [n_always + 4L, n_always + 4L + 4) (sentinel-padded to exactly kLeafMax).
+// [n_always + kLeafMax*L, n_always + kLeafMax*(L+1)) (sentinel-padded to exactly kLeafMax).
 struct alignas(16) Node {
     float lo0[3], hi0[3];
     float lo1[3], hi1[3];
@@ -35,7 +40,7 @@ static_assert(sizeof(Node) == 64, "node layout");
 struct Bvh {
     std::vector<Node> nodes;        // nodes[0] is the root
     std::vector<uint32_t> slot_to_sphere;  // leaf/always slot -> original sphere index
-    uint32_t n_always = 0;          // slots [0, n_always) are tested for every ray (unboundable spheres)
+    uint32_t n_always = 0;          // slots [0, n_always) are tested for every ray (unboundable + huge spheres)
     int depth = 0;
     double origin_bound = 0;        // rays with max|o_i| <= origin_bound are covered by the padding
     bool ok = false;

@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "rt_fastdiv.h"
+
 namespace rtk {
 
 constexpr int kBlock = 256;                // 4 waves of 64 lanes
@@ -46,15 +48,20 @@ struct KernelParams {
     uint32_t prof;   // 1: instrumented build, stats has 8 entries (see rt_context_enable_profile)
     uint32_t order;  // work-item order: 0 sample-major, 1 pixel-major (RTZIG_ORDER)
     uint32_t pad2;
+    FastDiv div_layer;  // / (n_rows * width): item -> (sample, pixel) in the refill
+    FastDiv div_width;  // / width: pixel -> (row, column)
 };
 
 // BVH (rt_bvh.hpp).  Node = both child boxes (f32, padded outward) + child refs; ref >= 0 is a
 // node index, ref < 0 the leaf ~ref.  Strides are ODD multiples of 16 B (node 80 B = 5 x 16, leaf
-// 144 B = 9 x 16) so that the per-lane random gathers (ds_read_b128) spread over all 16 bank slots
+// 2 slots: 80 B = 5 x 16) so that the per-lane random gathers (ds_read_b128) spread over all 16 bank slots
 // of the 256-B LDS row instead of piling onto 4 (64-B stride) or 2 (128-B stride) of them.
 constexpr int kBlockBvh = 512;     // 8 waves; 2 blocks per CU share the LDS budget
 constexpr int kMaxDepthBvh = 16;   // == rtbvh::kMaxDepth: per-lane LDS stack entries
-constexpr int kLeafBvh = 4;        // == rtbvh::kLeafMax: slots per (sentinel-padded) leaf
+#ifndef RTZIG_LEAF
+#define RTZIG_LEAF 2
+#endif
+constexpr int kLeafBvh = RTZIG_LEAF;       // == rtbvh::kLeafMax: slots per (sentinel-padded) leaf
 struct alignas(16) BvhNode {
     float lo0[3], hi0[3];
     float lo1[3], hi1[3];
@@ -62,13 +69,13 @@ struct alignas(16) BvhNode {
     int32_t pad[6];
 };  // 80 B
 struct alignas(16) LeafGeo {
-    double cx, cy, cz, r2;    // as GeoRec, 16-B aligned so that a leaf packs to 144 B
+    double cx, cy, cz, r2;    // as GeoRec, 16-B aligned so that a 2-slot leaf packs to 80 B
 };
 struct alignas(16) BvhLeaf {
     LeafGeo g[kLeafBvh];      // slot geometry (sentinels: {0,0,0,-inf})
     uint32_t sid[kLeafBvh];   // original sphere index per slot (0xffffffff for sentinels)
-};  // 144 B
-static_assert(sizeof(BvhNode) == 80 && sizeof(BvhLeaf) == 144, "BVH layouts");
+};  // 80 B for 2 slots (RTZIG_LEAF=4: 144 B)
+static_assert(sizeof(BvhNode) == 80 && sizeof(BvhLeaf) % 32 == 16, "BVH strides must be odd multiples of 16 B");
 struct BvhArgs {
     const BvhNode* nodes;
     const BvhLeaf* leaves;

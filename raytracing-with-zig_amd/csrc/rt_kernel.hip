@@ -272,7 +272,7 @@ struct BvhWalker {
             }
             if (cur != kDone) {
                 pr.leaf_iter();
-                // leaf: exactly kLeafBvh slots (sentinel-padded); the four discriminant chains
+                // leaf: exactly kLeafBvh slots (sentinel-padded); the kLeafBvh discriminant chains
                 // are independent, the candidate updates then run in slot order
                 const BvhLeaf* lf = leaves + (uint32_t)(~cur);
                 double h[kLeafBvh], disc[kLeafBvh];
@@ -365,14 +365,14 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
                     const uint32_t it32 = (uint32_t)item;
                     uint32_t s_local, q;
                     if (p.order == 0) {  // sample-major: a wave takes 64 neighbouring pixels
-                        s_local = it32 / P;
+                        s_local = fastdiv(it32, p.div_layer);
                         q = it32 - s_local * P;
                     } else {  // pixel-major: a wave takes consecutive samples of one pixel
                         q = it32 / p.s_count;
                         s_local = it32 - q * p.s_count;
                     }
                     slot = (uint64_t)s_local * P + q;
-                    const uint32_t row_local = q / W;
+                    const uint32_t row_local = fastdiv(q, p.div_width);
                     const uint32_t i = q - row_local * W;
                     const uint32_t j = p.row0 + row_local * p.row_step;
                     const uint64_t pixel = (uint64_t)j * W + i;

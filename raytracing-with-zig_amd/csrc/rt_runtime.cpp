@@ -235,6 +235,8 @@ rtk::KernelParams make_params(const rt_camera* c, uint32_t fmt, uint32_t row0, u
     p.n_rows = n_rows;
     p.n_spheres = n_spheres;
     p.n_pad = (n_spheres + rtk::kPad - 1) / rtk::kPad * rtk::kPad;
+    p.div_layer = rtk::fastdiv_make(n_rows * c->image_width);  // < 2^32 pixels (checked by callers)
+    p.div_width = rtk::fastdiv_make(c->image_width);
     (void)fmt;
     return p;
 }

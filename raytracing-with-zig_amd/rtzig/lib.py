@@ -77,6 +77,20 @@ def _declare(lib):
         fn.argtypes = args
 
 
+def _bind_torch_hip_runtime():
+    """One HIP runtime per process.  PyTorch-ROCm wheels bundle their own libamdhip64 (SONAME
+    libamdhip64.so.7, the same as /opt/rocm's) plus their own libhsa-runtime64, and torch's
+    libc10_hip NEEDs the unversioned name.  Loaded AFTER librtzig, torch therefore maps a second
+    HIP + ROCr stack next to ours, and that stack fails to initialise once our kernels have run
+    ("No HIP GPUs are available").  Loaded BEFORE, torch's runtime is the libamdhip64.so.7 the
+    dynamic linker hands librtzig too: both share one runtime, one device context and its streams.
+    Processes without torch (the Zig host, tools/rt_render_c) just use /opt/rocm's runtime."""
+    try:
+        import torch  # noqa: F401  (import only: maps torch's HIP runtime, does not init a GPU)
+    except ImportError:
+        pass
+
+
 def load():
     """Load librtzig.so (raises if it has not been built — there is no CPU fallback)."""
     global _lib
@@ -85,6 +99,7 @@ def load():
             raise RuntimeError(
                 f"{LIB_PATH} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
                 "(make -C raytracing-with-zig_amd/csrc)")
+        _bind_torch_hip_runtime()
         lib = C.CDLL(LIB_PATH)
         _declare(lib)
         _lib = lib

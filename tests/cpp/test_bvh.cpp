@@ -98,9 +98,9 @@ int main() {
         s.push_back(sph(INFINITY, 0, 0, 1));
         run(s, "soup");
     }
-    {  // large scene: depth bound must hold (median splits take over)
+    {  // large scene (15000 full leaves): depth bound must hold (median splits take over)
         std::vector<rt_sphere> s;
-        for (int k = 0; k < 60000; k++) s.push_back(sph(N(rng) * 10, N(rng), N(rng) * 10, 0.1));
+        for (int k = 0; k < 15000 * rtbvh::kLeafMax; k++) s.push_back(sph(N(rng) * 10, N(rng), N(rng) * 10, 0.1));
         run(s, "large");
     }
     std::printf(fails ? "FAILED %d\n" : "OK\n", fails);

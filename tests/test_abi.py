@@ -89,3 +89,18 @@ def test_invalid_arguments_fail_without_gpu_work():
     rc = lib.rt_render(C.byref(cam), (rtzig.RtSphere * 1)(rtzig.RtSphere(radius=1.0)), 1,
                        C.byref(opts), C.c_void_p(1))
     assert rc == abi.RT_ERR_INVALID
+
+
+def test_single_hip_runtime_per_process():
+    """rtzig loads torch's HIP runtime before librtzig (rtzig/lib.py), so a process that uses both
+    maps ONE libamdhip64 — a second runtime breaks torch's GPU init once our kernels have run."""
+    import subprocess
+    import sys
+    code = ("import sys; sys.path.insert(0, %r)\n"
+            "import rtzig; rtzig.load()\n"
+            "import torch\n"
+            "paths = {l.split()[-1] for l in open('/proc/self/maps') if 'libamdhip64' in l}\n"
+            "print(len(paths), sorted(paths))\n") % os.path.join(ROOT, "raytracing-with-zig_amd")
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr
+    assert out.stdout.startswith("1 "), out.stdout

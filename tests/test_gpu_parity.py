@@ -230,11 +230,16 @@ def test_walk_variants_bit_exact(oracle, variant, monkeypatch):
     assert np.array_equal(out, ref)
 
 
+@pytest.mark.parametrize("always_area", [None, "0", "1e-6"])
 @pytest.mark.parametrize("seed", [1, 2, 3])
-def test_bvh_random_scenes_bit_exact(oracle, seed, monkeypatch):
+def test_bvh_random_scenes_bit_exact(oracle, seed, always_area, monkeypatch):
     """BVH culling stress: random sphere soups (overlapping, duplicated, tiny and huge spheres,
-    negative radii) from random camera positions; the BVH walk must return the linear scan's bits."""
+    negative radii) from random camera positions; the BVH walk must return the linear scan's bits.
+    always_area: the builder's huge-sphere rule at its default, off, and nearly always on (the 4
+    largest spheres leave the tree for the always-list)."""
     monkeypatch.setenv("RTZIG_KERNEL", "bvh")
+    if always_area is not None:
+        monkeypatch.setenv("RTZIG_BVH_ALWAYS_AREA", always_area)
     rng = np.random.default_rng(seed)
     n = int(rng.integers(2, 300))
     arr = (RtSphere * (n + 2))()

@@ -2,7 +2,8 @@
 """A/B the sample-kernel variants IN ONE PROCESS, interleaved rounds (cdna guide rule 24).
 
     RTZIG_VARIANTS="1 2 4" python tools/ab_variants.py --spp 100 --rounds 5
-Each variant is selected through RTZIG_UNROLL (read at every launch).  Prints one JSON line with
+Each variant is selected through the --env variable (default RTZIG_UNROLL), set both while the
+variant's scene is built and at every launch.  Prints one JSON line with
 per-variant median/min sample-kernel ms (HIP events) and Msamples/s.
 """
 import argparse
@@ -28,17 +29,23 @@ args = ap.parse_args()
 
 cam = rtzig.final_scene_camera(width=args.width, aspect_ratio=args.aspect, spp=args.spp)
 H, W = cam.height, cam.width
-r = rtzig.DeviceRenderer(0)
-r.set_scene(cam.scene.world)
-r.enable_timing(True)
 out = torch.empty((H, W, 3), dtype=torch.float64, device="cuda:0")
 variants = args.variants.split()
+# one renderer per variant, with the variable set while the scene (and its BVH) is built too, so
+# the tool also A/Bs build-time knobs such as RTZIG_BVH_ALWAYS_AREA
+renderers = {}
+for v in variants:
+    os.environ[args.env] = v
+    renderers[v] = rtzig.DeviceRenderer(0)
+    renderers[v].set_scene(cam.scene.world)
+    renderers[v].enable_timing(True)
 times = {v: [] for v in variants}
 names = {}
 ref = None
 for rnd in range(args.rounds + 1):
     for v in variants:
         os.environ[args.env] = v
+        r = renderers[v]
         r.render_rows_async(cam.cam, out.data_ptr())
         torch.cuda.synchronize()
         sm, _ = r.kernel_times()
