@@ -97,10 +97,19 @@ struct Rng {
     }
     // Random.float(f64) (zig std/Random.zig): mantissa = low 52 bits, exponent from leading zeros;
     // >= 12 leading zeros (p = 1/4096) pulls further draws.
+    // Fast path on 32-bit halves: fewer than 12 leading zeros <=> hi >= 2^20, and then the leading
+    // one lies in hi, so lz = clz(hi) and the high word of the result is bfi(0xfffff, hi, e << 20).
     __device__ __forceinline__ double uniform() {
         const uint64_t rnd = next();
+        const uint32_t hi = (uint32_t)(rnd >> 32);
+        if (__builtin_expect(hi < (1u << 20), 0)) return uniform_slow(rnd);
+        const uint32_t e = 1022u - (uint32_t)__builtin_clz(hi);
+        const uint32_t ohi = (e << 20) | (hi & 0xfffffu);
+        return __builtin_bit_cast(double, ((uint64_t)ohi << 32) | (uint32_t)rnd);
+    }
+    __device__ __forceinline__ double uniform_slow(uint64_t rnd) {  // p = 2^-12 per draw
         uint64_t lz = rnd ? (uint64_t)__builtin_clzll(rnd) : 64;
-        if (__builtin_expect(lz >= 12, 0)) {
+        if (lz >= 12) {
             lz = 12;
             for (;;) {
                 const uint64_t w = next();
@@ -115,6 +124,9 @@ struct Rng {
     }
     // util.randomDoubleRange (util.zig:20-22)
     __device__ __forceinline__ double range(double mn, double mx) { return mn + (mx - mn) * uniform(); }
+    // range(-1, 1): (1 - -1) * u = 2u is exact, so -1 + 2u has ONE rounding and fma(2, u, -1) gives
+    // the same bits with one f64 op instead of two (u may be subnormal: 2u is still exact).
+    __device__ __forceinline__ double range_pm1() { return __builtin_fma(2.0, uniform(), -1.0); }
 };
 
 // key(seed, pixel, sample) = mix(mix(seed) ^ (pixel << 32 | sample)); seed_mix = mix(seed) is
@@ -127,16 +139,16 @@ __device__ __forceinline__ uint64_t sample_key(uint64_t seed_mix, uint64_t pixel
 __device__ __forceinline__ v3 random_unit_vec(Rng& g) {
 #ifdef RTZIG_ABLATE_RUV  // timing ablation only (wrong distribution): one candidate, no loop
     {
-        const double x = g.range(-1, 1), y = g.range(-1, 1), z = g.range(-1, 1);
+        const double x = g.range_pm1(), y = g.range_pm1(), z = g.range_pm1();
         const double ls = (x * x + y * y) + z * z;
         const double l = __builtin_sqrt(ls > 1e-160 ? ls : 1.0);
         return v3{x / l, y / l, z / l};
     }
 #endif
     for (;;) {
-        const double x = g.range(-1, 1);
-        const double y = g.range(-1, 1);
-        const double z = g.range(-1, 1);
+        const double x = g.range_pm1();
+        const double y = g.range_pm1();
+        const double z = g.range_pm1();
         const double ls = (x * x + y * y) + z * z;
         if (1e-160 < ls && ls <= 1) {
             const double l = __builtin_sqrt(ls);
@@ -148,8 +160,8 @@ __device__ __forceinline__ v3 random_unit_vec(Rng& g) {
 // Vec.randomInUnitDisk (vec.zig:82-92)
 __device__ __forceinline__ v3 random_in_unit_disk(Rng& g) {
     for (;;) {
-        const double x = g.range(-1, 1);
-        const double y = g.range(-1, 1);
+        const double x = g.range_pm1();
+        const double y = g.range_pm1();
         if ((x * x + y * y) + 0.0 * 0.0 < 1) return v3{x, y, 0.0};
     }
 }
