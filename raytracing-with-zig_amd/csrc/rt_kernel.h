@@ -52,8 +52,8 @@ struct KernelParams {
     FastDiv div_width;  // / width: pixel -> (row, column)
 };
 
-// BVH (rt_bvh.hpp).  Node = both child boxes (f32, padded outward) + child refs; ref >= 0 is a
-// node index, ref < 0 the leaf ~ref.  Strides are ODD multiples of 16 B (node 80 B = 5 x 16, leaf
+// BVH (rt_bvh.hpp).  Node = both child boxes (f32, padded outward) + child refs; on the device a
+// ref >= 0 is the BYTE offset of a node, ref < 0 is ~(byte offset of a leaf block).  Strides are ODD multiples of 16 B (node 80 B = 5 x 16, leaf
 // 2 slots: 80 B = 5 x 16) so that the per-lane random gathers (ds_read_b128) spread over all 16 bank slots
 // of the 256-B LDS row instead of piling onto 4 (64-B stride) or 2 (128-B stride) of them.
 constexpr int kBlockBvh = 512;     // 8 waves; 2 blocks per CU share the LDS budget

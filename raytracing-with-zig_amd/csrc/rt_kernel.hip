@@ -156,6 +156,23 @@ struct LinearWalker {
     }
 };
 
+// Slab-interval ends: max(x, y, z, lower) and min(x, y, z, upper) as hardware v_max3/v_min3 +
+// v_max/v_min.  With IEEE mode on (the default) these return the non-NaN operand for quiet NaNs —
+// exactly fmaxf/fminf on every value this walk produces (arithmetic never yields signaling NaNs) —
+// but written as builtins the compiler re-canonicalizes the loop-carried bounds every iteration.
+__device__ __forceinline__ float slab_near(float x, float y, float z, float lower) {
+    float t, r;
+    asm volatile("v_max_f32 %0, %1, %2" : "=v"(t) : "v"(z), "v"(lower));
+    asm volatile("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(x), "v"(y), "v"(t));
+    return r;
+}
+__device__ __forceinline__ float slab_far(float x, float y, float z, float upper) {
+    float t, r;
+    asm volatile("v_min_f32 %0, %1, %2" : "=v"(t) : "v"(z), "v"(upper));
+    asm volatile("v_min3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(x), "v"(y), "v"(t));
+    return r;
+}
+
 // BVH walk (rt_bvh.hpp): per-lane, near-child-first, stack in LDS.  Every visited sphere runs the
 // same f64 quadratic as the linear walk; the candidate root of sphere k is
 //   t_k = root1 if t_min < root1, else root2 if t_min < root2   (sphere.zig:38-41),
@@ -233,23 +250,19 @@ struct BvhWalker {
             while (cur >= 0) {
                 pr.visit();
                 pr.inner_iter();
-                const BvhNode nd = nodes[cur];
+                const BvhNode nd = *(const BvhNode*)((const char*)nodes + cur);  // byte-offset ref
                 float n0, f0, n1, f1;
                 {
                     const float ax0 = __builtin_fmaf(nd.lo0[0], ix, -oix), bx0 = __builtin_fmaf(nd.hi0[0], ix, -oix);
                     const float ay0 = __builtin_fmaf(nd.lo0[1], iy, -oiy), by0 = __builtin_fmaf(nd.hi0[1], iy, -oiy);
                     const float az0 = __builtin_fmaf(nd.lo0[2], iz, -oiz), bz0 = __builtin_fmaf(nd.hi0[2], iz, -oiz);
-                    n0 = __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(ax0, bx0), __builtin_fminf(ay0, by0)),
-                                         __builtin_fmaxf(__builtin_fminf(az0, bz0), lower));
-                    f0 = __builtin_fminf(__builtin_fminf(__builtin_fmaxf(ax0, bx0), __builtin_fmaxf(ay0, by0)),
-                                         __builtin_fminf(__builtin_fmaxf(az0, bz0), upper));
+                    n0 = slab_near(__builtin_fminf(ax0, bx0), __builtin_fminf(ay0, by0), __builtin_fminf(az0, bz0), lower);
+                    f0 = slab_far(__builtin_fmaxf(ax0, bx0), __builtin_fmaxf(ay0, by0), __builtin_fmaxf(az0, bz0), upper);
                     const float ax1 = __builtin_fmaf(nd.lo1[0], ix, -oix), bx1 = __builtin_fmaf(nd.hi1[0], ix, -oix);
                     const float ay1 = __builtin_fmaf(nd.lo1[1], iy, -oiy), by1 = __builtin_fmaf(nd.hi1[1], iy, -oiy);
                     const float az1 = __builtin_fmaf(nd.lo1[2], iz, -oiz), bz1 = __builtin_fmaf(nd.hi1[2], iz, -oiz);
-                    n1 = __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(ax1, bx1), __builtin_fminf(ay1, by1)),
-                                         __builtin_fmaxf(__builtin_fminf(az1, bz1), lower));
-                    f1 = __builtin_fminf(__builtin_fminf(__builtin_fmaxf(ax1, bx1), __builtin_fmaxf(ay1, by1)),
-                                         __builtin_fminf(__builtin_fmaxf(az1, bz1), upper));
+                    n1 = slab_near(__builtin_fminf(ax1, bx1), __builtin_fminf(ay1, by1), __builtin_fminf(az1, bz1), lower);
+                    f1 = slab_far(__builtin_fmaxf(ax1, bx1), __builtin_fmaxf(ay1, by1), __builtin_fmaxf(az1, bz1), upper);
                 }
                 const bool h0 = n0 <= f0;
                 const bool h1 = n1 <= f1;
@@ -274,7 +287,7 @@ struct BvhWalker {
                 pr.leaf_iter();
                 // leaf: exactly kLeafBvh slots (sentinel-padded); the kLeafBvh discriminant chains
                 // are independent, the candidate updates then run in slot order
-                const BvhLeaf* lf = leaves + (uint32_t)(~cur);
+                const BvhLeaf* lf = (const BvhLeaf*)((const char*)leaves + (uint32_t)(~cur));
                 double h[kLeafBvh], disc[kLeafBvh];
 #pragma unroll
                 for (int u = 0; u < kLeafBvh; ++u) {

@@ -125,12 +125,21 @@ int ensure_buffer(void** ptr, size_t* bytes, size_t need) {
     return RT_OK;
 }
 
+// Builder ref (node index >= 0, ~leaf index < 0) -> device ref (byte offsets, see upload_bvh).
+int32_t device_ref(int32_t ref) {
+    if (ref >= 0) return (int32_t)((int64_t)ref * (int64_t)sizeof(rtk::BvhNode));
+    return ~(int32_t)((int64_t)(~ref) * (int64_t)sizeof(rtk::BvhLeaf));
+}
+
 // Builds and uploads the BVH for the context's scene, valid for ray origins with |o_i| <= bound.
 int upload_bvh(rt_context* ctx, double bound) {
     const rtbvh::Bvh bvh = rtbvh::build(ctx->spheres.data(), ctx->spheres.size(), bound);
-    ctx->bvh_ok = bvh.ok;
+    // byte-offset refs must fit int32 (and stay clear of the walk's INT32_MIN "done" marker)
+    const bool fits = bvh.nodes.size() * sizeof(rtk::BvhNode) < (1ull << 30) &&
+                      bvh.slot_to_sphere.size() / rtk::kLeafBvh * sizeof(rtk::BvhLeaf) < (1ull << 30);
+    ctx->bvh_ok = bvh.ok && fits;
     ctx->bvh_origin_bound = bound;
-    if (!bvh.ok) return RT_OK;
+    if (!ctx->bvh_ok) return RT_OK;
     static_assert(rtbvh::kLeafMax == rtk::kLeafBvh && rtbvh::kMaxDepth == rtk::kMaxDepthBvh, "BVH constants differ");
     const size_t nn = bvh.nodes.size();
     const size_t na = bvh.n_always;
@@ -161,8 +170,10 @@ int upload_bvh(rt_context* ctx, double bound) {
             d.lo1[a] = src.lo1[a];
             d.hi1[a] = src.hi1[a];
         }
-        d.ref0 = src.ref0;
-        d.ref1 = src.ref1;
+        // device refs are BYTE offsets (node: ref * 80 >= 0, leaf: ~(leaf * sizeof(BvhLeaf))) so the
+        // walk forms LDS/global addresses with an add instead of a quarter-rate v_mul_lo_u32
+        d.ref0 = device_ref(src.ref0);
+        d.ref1 = device_ref(src.ref1);
     }
     std::vector<rtk::BvhLeaf> leaves(nl ? nl : 1);
     for (size_t l = 0; l < nl; l++)
