@@ -145,16 +145,18 @@ __device__ __forceinline__ v3 random_unit_vec(Rng& g) {
         return v3{x / l, y / l, z / l};
     }
 #endif
-    for (;;) {
-        const double x = g.range_pm1();
-        const double y = g.range_pm1();
-        const double z = g.range_pm1();
-        const double ls = (x * x + y * y) + z * z;
-        if (1e-160 < ls && ls <= 1) {
-            const double l = __builtin_sqrt(ls);
-            return v3{x / l, y / l, z / l};
-        }
-    }
+    // The loop only draws candidates; the sqrt and the three divisions run once, after it.
+    // (Written with the return inside the loop, the compiler keeps them in the loop body, and a
+    // wave executes them on every trip in which any lane accepts: ~5 times per call.)
+    double x, y, z, ls;
+    do {
+        x = g.range_pm1();
+        y = g.range_pm1();
+        z = g.range_pm1();
+        ls = (x * x + y * y) + z * z;
+    } while (!(1e-160 < ls && ls <= 1));
+    const double l = __builtin_sqrt(ls);
+    return v3{x / l, y / l, z / l};
 }
 
 // Vec.randomInUnitDisk (vec.zig:82-92)

@@ -53,21 +53,25 @@ struct KernelParams {
 };
 
 // BVH (rt_bvh.hpp).  Node = both child boxes (f32, padded outward) + child refs; on the device a
-// ref >= 0 is the BYTE offset of a node, ref < 0 is ~(byte offset of a leaf block).  Strides are ODD multiples of 16 B (node 80 B = 5 x 16, leaf
-// 2 slots: 80 B = 5 x 16) so that the per-lane random gathers (ds_read_b128) spread over all 16 bank slots
-// of the 256-B LDS row instead of piling onto 4 (64-B stride) or 2 (128-B stride) of them.
+// ref >= 0 is the BYTE offset of a node, ref < 0 is ~(byte offset of a leaf block).
+// Each axis of each child box is stored as {lo, hi, hi, lo}: a lane reads the 8-B pair at +0
+// (lo, hi) when its ray direction on that axis is >= 0 and at +8 (hi, lo) when it is < 0, so one
+// ds_read_b64 delivers (near plane, far plane) in ray order and the slab test needs no per-axis
+// min/max (rt_kernel.hip, BvhWalker).  Node stride 104 B = 26 dwords: consecutive nodes start
+// on 32 different banks of the 64 (gcd(26, 64) = 2), so per-lane random ds_read_b64 gathers
+// spread over the whole bank row.  Leaves (2 slots: 80 B = 5 x 16, read as ds_read_b128) start
+// at the next 16-B boundary after the nodes.
 constexpr int kBlockBvh = 512;     // 8 waves; 2 blocks per CU share the LDS budget
-constexpr int kMaxDepthBvh = 16;   // == rtbvh::kMaxDepth: per-lane LDS stack entries
+constexpr int kMaxDepthBvh = 16;   // == rtbvh::kMaxDepth: bound on per-lane LDS stack entries (entry 0: "done")
 #ifndef RTZIG_LEAF
 #define RTZIG_LEAF 2
 #endif
 constexpr int kLeafBvh = RTZIG_LEAF;       // == rtbvh::kLeafMax: slots per (sentinel-padded) leaf
-struct alignas(16) BvhNode {
-    float lo0[3], hi0[3];
-    float lo1[3], hi1[3];
+struct alignas(8) BvhNode {
+    float c0[3][4];   // child 0: per axis {lo, hi, hi, lo}
+    float c1[3][4];   // child 1
     int32_t ref0, ref1;
-    int32_t pad[6];
-};  // 80 B
+};  // 104 B
 struct alignas(16) LeafGeo {
     double cx, cy, cz, r2;    // as GeoRec, 16-B aligned so that a 2-slot leaf packs to 80 B
 };
@@ -75,14 +79,19 @@ struct alignas(16) BvhLeaf {
     LeafGeo g[kLeafBvh];      // slot geometry (sentinels: {0,0,0,-inf})
     uint32_t sid[kLeafBvh];   // original sphere index per slot (0xffffffff for sentinels)
 };  // 80 B for 2 slots (RTZIG_LEAF=4: 144 B)
-static_assert(sizeof(BvhNode) == 80 && sizeof(BvhLeaf) % 32 == 16, "BVH strides must be odd multiples of 16 B");
+static_assert(sizeof(BvhNode) == 104 && sizeof(BvhLeaf) % 32 == 16, "BVH node / leaf strides (bank spread)");
 struct BvhArgs {
     const BvhNode* nodes;
     const BvhLeaf* leaves;
     const GeoRec* always_geo;    // spheres tested for every ray (unboundable)
     const uint32_t* always_sid;
-    uint32_t n_nodes, n_leaves, n_always, pad;
+    uint32_t n_nodes, n_leaves, n_always;
+    uint32_t stack_depth;  // per-lane stack entries the tree needs: its depth (root = 1), <= kMaxDepthBvh
 };
+// LDS layout of the BVH kernel: [nodes, padded to 16 B][leaves][stacks: stack_depth x kBlockBvh x 4 B]
+__host__ __device__ inline uint32_t bvh_leaves_offset(uint32_t n_nodes) {
+    return (n_nodes * (uint32_t)sizeof(BvhNode) + 15u) & ~15u;
+}
 
 // Arguments of the ordered reduction: pixel q's running sum += samples[s][q] for s = 0..s_count-1
 // (exactly the reference's sequential `pixelColor += rayColor(ray)`, camera.zig:133-136).

@@ -177,6 +177,25 @@ __device__ __forceinline__ float slab_far(float x, float y, float z, float upper
 // same f64 quadratic as the linear walk; the candidate root of sphere k is
 //   t_k = root1 if t_min < root1, else root2 if t_min < root2   (sphere.zig:38-41),
 // and it wins iff t_k < closest, or t_k == closest and k is lower (the linear scan's first-wins).
+constexpr int32_t kDone = INT32_MIN;  // walk finished (stack entry 0)
+typedef float f2 __attribute__((ext_vector_type(2)));
+typedef int32_t i2 __attribute__((ext_vector_type(2)));
+
+// LDS reads issued as single instructions (the caller waits with s_waitcnt lgkmcnt(0), naming the
+// results as operands so nothing reads them earlier).  `addr` is an LDS byte address.
+template <class T>
+__device__ __forceinline__ void lds_b64(T& v, uint32_t addr, int off) {
+    static_assert(sizeof(T) == 8, "b64");
+    asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "i"(off));
+}
+__device__ __forceinline__ void lds_b32(int32_t& v, uint32_t addr, int off) {
+    asm volatile("ds_read_b32 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "i"(off));
+}
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
+
+template <bool kLdsNodes>
 struct BvhWalker {
     const BvhNode* __restrict__ nodes;
     const BvhLeaf* __restrict__ leaves;
@@ -232,56 +251,76 @@ struct BvhWalker {
         if (__builtin_fabsf(dz) < 1e-30f) dz = __builtin_copysignf(1e-30f, dz);
         const float ix = 1.0f / dx, iy = 1.0f / dy, iz = 1.0f / dz;
         // slab planes as t = fma(bound, inv, -o*inv): one op per plane.  Error (position space,
-        // per axis) <= 2^-24 (3|bound| + 4|o|), inside the padding of rt_bvh.cpp; overflowed
-        // planes give inf/NaN, and NaN operands are dropped by fminf/fmaxf (permissive, so safe).
-        const float oix = ox * ix, oiy = oy * iy, oiz = oz * iz;
+        // per axis) <= 2^-24 (3|bound| + 4|o|), inside the padding of rt_bvh.cpp.  fma is monotone
+        // in `bound`, so for inv > 0 the lo plane is the near one and for inv < 0 the hi plane: the
+        // lane reads its (near, far) pair per axis at byte +0 or +8 of the axis's {lo, hi, hi, lo}
+        // (rtk::BvhNode) and both planes of an axis come out of one packed fma.  inv is never 0 or
+        // NaN (|d| >= 1e-30), so the pick matches the min/max of the two planes exactly; an
+        // overflowed plane is +-inf in ray order, and NaN arises only from a NaN origin, which
+        // v_max3/v_min3 drop (the box is kept: permissive, never a wrong cull).
+        const uint32_t ax = ix < 0 ? 8u : 0u, ay = 16u + (iy < 0 ? 8u : 0u), az = 32u + (iz < 0 ? 8u : 0u);
+        const f2 inv_x = {ix, ix}, inv_y = {iy, iy}, inv_z = {iz, iz};
+        const f2 noi_x = {-(ox * ix), -(ox * ix)}, noi_y = {-(oy * iy), -(oy * iy)}, noi_z = {-(oz * iz), -(oz * iz)};
         float lower = (float)t_min;
         lower = lower - __builtin_fabsf(lower) * 0x1p-20f - 1e-30f;
         float upper = (float)closest;
         upper = upper + __builtin_fabsf(upper) * 0x1p-20f;
 
+        // stack: entry 0 holds kDone (written once per lane at kernel start), entries 1..sp the
+        // pushed far children; a pop reads entry sp, so popping the empty stack yields kDone
         int sp = 0;
         int32_t cur = 0;  // root
         // while-while (Aila & Laine 2009): every lane advances through internal nodes until it
         // holds a leaf (or is done); then the lanes with a leaf test its spheres together, so the
         // f64 leaf work runs with most lanes active instead of whenever any one lane hits a leaf.
-        constexpr int32_t kDone = INT32_MIN;
         while (cur != kDone) {
             while (cur >= 0) {
                 pr.visit();
                 pr.inner_iter();
-                const BvhNode nd = *(const BvhNode*)((const char*)nodes + cur);  // byte-offset ref
-                float n0, f0, n1, f1;
-                {
-                    const float ax0 = __builtin_fmaf(nd.lo0[0], ix, -oix), bx0 = __builtin_fmaf(nd.hi0[0], ix, -oix);
-                    const float ay0 = __builtin_fmaf(nd.lo0[1], iy, -oiy), by0 = __builtin_fmaf(nd.hi0[1], iy, -oiy);
-                    const float az0 = __builtin_fmaf(nd.lo0[2], iz, -oiz), bz0 = __builtin_fmaf(nd.hi0[2], iz, -oiz);
-                    n0 = slab_near(__builtin_fminf(ax0, bx0), __builtin_fminf(ay0, by0), __builtin_fminf(az0, bz0), lower);
-                    f0 = slab_far(__builtin_fmaxf(ax0, bx0), __builtin_fmaxf(ay0, by0), __builtin_fmaxf(az0, bz0), upper);
-                    const float ax1 = __builtin_fmaf(nd.lo1[0], ix, -oix), bx1 = __builtin_fmaf(nd.hi1[0], ix, -oix);
-                    const float ay1 = __builtin_fmaf(nd.lo1[1], iy, -oiy), by1 = __builtin_fmaf(nd.hi1[1], iy, -oiy);
-                    const float az1 = __builtin_fmaf(nd.lo1[2], iz, -oiz), bz1 = __builtin_fmaf(nd.hi1[2], iz, -oiz);
-                    n1 = slab_near(__builtin_fminf(ax1, bx1), __builtin_fminf(ay1, by1), __builtin_fminf(az1, bz1), lower);
-                    f1 = slab_far(__builtin_fmaxf(ax1, bx1), __builtin_fmaxf(ay1, by1), __builtin_fmaxf(az1, bz1), upper);
+                int32_t* top = stack + sp * kBlockBvh;
+                f2 bx0, by0, bz0, bx1, by1, bz1;
+                int32_t ref0, ref1, popped;
+                if constexpr (kLdsNodes) {
+                    // nodes start at LDS address 0: the ref is the address.  Seven ds_read_b64
+                    // (2 LDS cycles each); left to itself the compiler pairs them into
+                    // ds_read2_b64 (8 cycles for the same 16 B) behind extra base adds.
+                    const uint32_t a = (uint32_t)cur;
+                    i2 refs;
+                    lds_b64(bx0, a + ax, 0); lds_b64(bx1, a + ax, 48);
+                    lds_b64(by0, a + ay, 0); lds_b64(by1, a + ay, 48);
+                    lds_b64(bz0, a + az, 0); lds_b64(bz1, a + az, 48);
+                    lds_b64(refs, a, 96);
+                    lds_b32(popped, lds_addr(top), 0);
+                    asm volatile("s_waitcnt lgkmcnt(0)"
+                                 : "+v"(bx0), "+v"(bx1), "+v"(by0), "+v"(by1), "+v"(bz0), "+v"(bz1), "+v"(refs),
+                                   "+v"(popped));
+                    ref0 = refs.x;
+                    ref1 = refs.y;
+                } else {
+                    const char* nb = (const char*)nodes + cur;  // byte-offset ref
+                    bx0 = *(const f2*)(nb + ax); by0 = *(const f2*)(nb + ay); bz0 = *(const f2*)(nb + az);
+                    bx1 = *(const f2*)(nb + 48 + ax); by1 = *(const f2*)(nb + 48 + ay); bz1 = *(const f2*)(nb + 48 + az);
+                    ref0 = *(const int32_t*)(nb + 96);
+                    ref1 = *(const int32_t*)(nb + 100);
+                    popped = *top;
                 }
+                const f2 tx0 = __builtin_elementwise_fma(bx0, inv_x, noi_x);
+                const f2 ty0 = __builtin_elementwise_fma(by0, inv_y, noi_y);
+                const f2 tz0 = __builtin_elementwise_fma(bz0, inv_z, noi_z);
+                const f2 tx1 = __builtin_elementwise_fma(bx1, inv_x, noi_x);
+                const f2 ty1 = __builtin_elementwise_fma(by1, inv_y, noi_y);
+                const f2 tz1 = __builtin_elementwise_fma(bz1, inv_z, noi_z);
+                const float n0 = slab_near(tx0.x, ty0.x, tz0.x, lower), f0 = slab_far(tx0.y, ty0.y, tz0.y, upper);
+                const float n1 = slab_near(tx1.x, ty1.x, tz1.x, lower), f1 = slab_far(tx1.y, ty1.y, tz1.y, upper);
                 const bool h0 = n0 <= f0;
                 const bool h1 = n1 <= f1;
                 // both hit: descend into the nearer child and push the farther one (the store
                 // always happens; it only counts when sp advances); one hit: descend; none: pop
                 const bool first0 = n0 <= n1;
-                const int32_t near_ref = first0 ? nd.ref0 : nd.ref1;
-                const int32_t far_ref = first0 ? nd.ref1 : nd.ref0;
-                stack[sp * kBlockBvh] = far_ref;
-                const bool both = h0 && h1;
-                sp += both ? 1 : 0;
-                if (h0 || h1) {
-                    cur = both ? near_ref : (h0 ? nd.ref0 : nd.ref1);
-                } else if (sp == 0) {
-                    cur = kDone;
-                } else {
-                    --sp;
-                    cur = stack[sp * kBlockBvh];
-                }
+                top[kBlockBvh] = first0 ? ref1 : ref0;
+                const bool pick0 = h0 && (!h1 || first0);  // both: nearer; one: that one
+                cur = (h0 || h1) ? (pick0 ? ref0 : ref1) : popped;
+                sp = sp + (int)(h0 && h1) - (int)!(h0 || h1);
             }
             if (cur != kDone) {
                 pr.leaf_iter();
@@ -306,12 +345,8 @@ struct BvhWalker {
                 pr.tests(kLeafBvh);
                 upper = (float)closest;
                 upper = upper + __builtin_fabsf(upper) * 0x1p-20f;
-                if (sp == 0) {
-                    cur = kDone;
-                } else {
-                    --sp;
-                    cur = stack[sp * kBlockBvh];
-                }
+                cur = stack[sp * kBlockBvh];  // pop (entry 0: kDone)
+                --sp;
             }
         }
         *t_hit = closest;
@@ -557,21 +592,25 @@ __global__ __launch_bounds__(kBlockBvh) void sample_kernel_bvh(KernelParams p, B
                                                                double* __restrict__ samples,
                                                                unsigned long long* __restrict__ queue,
                                                                unsigned long long* __restrict__ stats) {
+    // LDS: [nodes][leaves] (kLdsScene) at address 0, so a node's byte-offset ref IS its LDS
+    // address; then the per-lane stacks [kMaxDepthBvh][kBlockBvh]
     extern __shared__ __align__(16) unsigned char lds_raw[];
-    int32_t* stack = (int32_t*)lds_raw;  // [kMaxDepthBvh][kBlockBvh]
-    unsigned char* scene = lds_raw + (size_t)kMaxDepthBvh * kBlockBvh * sizeof(int32_t);
+    const size_t scene_bytes =
+        kLdsScene ? (size_t)bvh_leaves_offset(b.n_nodes) + (size_t)b.n_leaves * sizeof(BvhLeaf) : 0;
+    int32_t* stack = (int32_t*)(lds_raw + scene_bytes);
+    stack[threadIdx.x] = kDone;  // entry 0 of this lane's stack: popping it ends the walk
     const BvhNode* nodes = b.nodes;
     const BvhLeaf* leaves = b.leaves;
     if constexpr (kLdsScene) {
-        BvhNode* ln = (BvhNode*)scene;
-        BvhLeaf* ll = (BvhLeaf*)(scene + (size_t)b.n_nodes * sizeof(BvhNode));
+        BvhNode* ln = (BvhNode*)lds_raw;
+        BvhLeaf* ll = (BvhLeaf*)(lds_raw + bvh_leaves_offset(b.n_nodes));
         for (uint32_t k = threadIdx.x; k < b.n_nodes; k += blockDim.x) ln[k] = b.nodes[k];
         for (uint32_t k = threadIdx.x; k < b.n_leaves; k += blockDim.x) ll[k] = b.leaves[k];
         __syncthreads();
         nodes = ln;
         leaves = ll;
     }
-    path_loop<kProf>(p, BvhWalker{nodes, leaves, b.always_geo, b.always_sid, b.n_always, stack + threadIdx.x}, geo_g,
+    path_loop<kProf>(p, BvhWalker<kLdsScene>{nodes, leaves, b.always_geo, b.always_sid, b.n_always, stack + threadIdx.x}, geo_g,
                      mat_g, samples, queue, stats);
 }
 
@@ -702,8 +741,9 @@ extern "C" hipError_t rtk_launch_samples_bvh(const rtk::KernelParams* p, const r
     using namespace rtk;
     const uint64_t total = (uint64_t)p->n_rows * p->width * p->s_count;
     if (total == 0) return hipSuccess;
-    const size_t stack_bytes = (size_t)kMaxDepthBvh * kBlockBvh * sizeof(int32_t);
-    const size_t scene_bytes = (size_t)b->n_nodes * sizeof(BvhNode) + (size_t)b->n_leaves * sizeof(BvhLeaf);
+    if (b->stack_depth < 2 || b->stack_depth > (uint32_t)kMaxDepthBvh) return hipErrorInvalidValue;
+    const size_t stack_bytes = (size_t)b->stack_depth * kBlockBvh * sizeof(int32_t);
+    const size_t scene_bytes = (size_t)bvh_leaves_offset(b->n_nodes) + (size_t)b->n_leaves * sizeof(BvhLeaf);
     // scene in LDS when two blocks (16 waves) still fit a CU's 160 KiB
     const bool lds_scene = stack_bytes + scene_bytes <= 80 * 1024;
     const size_t shmem = stack_bytes + (lds_scene ? scene_bytes : 0);

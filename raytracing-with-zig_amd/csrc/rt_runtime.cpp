@@ -164,13 +164,13 @@ int upload_bvh(rt_context* ctx, double bound) {
         const rtbvh::Node& src = bvh.nodes[i];
         rtk::BvhNode& d = nodes[i];
         std::memset(&d, 0, sizeof d);
-        for (int a = 0; a < 3; a++) {
-            d.lo0[a] = src.lo0[a];
-            d.hi0[a] = src.hi0[a];
-            d.lo1[a] = src.lo1[a];
-            d.hi1[a] = src.hi1[a];
+        for (int a = 0; a < 3; a++) {  // {lo, hi, hi, lo}: see rtk::BvhNode
+            d.c0[a][0] = d.c0[a][3] = src.lo0[a];
+            d.c0[a][1] = d.c0[a][2] = src.hi0[a];
+            d.c1[a][0] = d.c1[a][3] = src.lo1[a];
+            d.c1[a][1] = d.c1[a][2] = src.hi1[a];
         }
-        // device refs are BYTE offsets (node: ref * 80 >= 0, leaf: ~(leaf * sizeof(BvhLeaf))) so the
+        // device refs are BYTE offsets (node: ref * 104 >= 0, leaf: ~(leaf * sizeof(BvhLeaf))) so the
         // walk forms LDS/global addresses with an add instead of a quarter-rate v_mul_lo_u32
         d.ref0 = device_ref(src.ref0);
         d.ref1 = device_ref(src.ref1);
@@ -209,6 +209,7 @@ int upload_bvh(rt_context* ctx, double bound) {
     ctx->bvh.n_nodes = (uint32_t)nn;
     ctx->bvh.n_leaves = (uint32_t)nl;
     ctx->bvh.n_always = (uint32_t)na;
+    ctx->bvh.stack_depth = (uint32_t)std::max(2, std::min(bvh.depth, rtk::kMaxDepthBvh));
     return RT_OK;
 }
 
