@@ -135,28 +135,14 @@ __device__ __forceinline__ uint64_t sample_key(uint64_t seed_mix, uint64_t pixel
     return sm_mix_hd(seed_mix ^ ((pixel << 32) | (uint64_t)sample));
 }
 
-// Vec.randomUnitVec (vec.zig:71-80): rejection in the cube, then TRUE division by the length.
-__device__ __forceinline__ v3 random_unit_vec(Rng& g) {
-#ifdef RTZIG_ABLATE_RUV  // timing ablation only (wrong distribution): one candidate, no loop
-    {
-        const double x = g.range_pm1(), y = g.range_pm1(), z = g.range_pm1();
-        const double ls = (x * x + y * y) + z * z;
-        const double l = __builtin_sqrt(ls > 1e-160 ? ls : 1.0);
-        return v3{x / l, y / l, z / l};
-    }
-#endif
-    // The loop only draws candidates; the sqrt and the three divisions run once, after it.
-    // (Written with the return inside the loop, the compiler keeps them in the loop body, and a
-    // wave executes them on every trip in which any lane accepts: ~5 times per call.)
-    double x, y, z, ls;
-    do {
-        x = g.range_pm1();
-        y = g.range_pm1();
-        z = g.range_pm1();
-        ls = (x * x + y * y) + z * z;
-    } while (!(1e-160 < ls && ls <= 1));
-    const double l = __builtin_sqrt(ls);
-    return v3{x / l, y / l, z / l};
+// One trip of Vec.randomUnitVec's rejection loop (vec.zig:73-79): draws a candidate in the cube and
+// returns whether it is accepted.  The caller finishes with p / sqrt(|p|^2) (true division).
+__device__ __forceinline__ bool ruv_candidate(Rng& g, double& x, double& y, double& z, double& ls) {
+    x = g.range_pm1();
+    y = g.range_pm1();
+    z = g.range_pm1();
+    ls = (x * x + y * y) + z * z;
+    return 1e-160 < ls && ls <= 1;
 }
 
 // Vec.randomInUnitDisk (vec.zig:82-92)

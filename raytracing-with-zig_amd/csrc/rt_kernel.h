@@ -12,6 +12,10 @@ constexpr int kBlock = 256;                // 4 waves of 64 lanes
 constexpr uint32_t kMaxLdsSpheres = 2048;  // 64 KiB of LDS geometry; above this, read from global
 constexpr uint32_t kChunk = 2048;          // work items a wave claims per queue fetch
 constexpr uint32_t kPad = 4;               // sphere list padded to a multiple of this (sentinels)
+#ifndef RTZIG_RUV_TRIPS
+#define RTZIG_RUV_TRIPS 3
+#endif
+constexpr int kRuvTrips = RTZIG_RUV_TRIPS;  // randomUnitVec rejection trips per loop iteration (path_loop)
 constexpr const char* kDefaultVariant = "smem_u4";  // see variant_choice() in rt_kernel.hip
 
 // Geometry walked by every lane for every ray: 32 B, one LDS broadcast pair per sphere.

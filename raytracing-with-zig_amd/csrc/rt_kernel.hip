@@ -410,6 +410,10 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
     Ray r;
     v3 att = mk(1, 1, 1);
     uint32_t bounce = 0;
+    // pending Lambertian/Metal scatter (waiting for its randomUnitVec), see below
+    bool pending = false, sc_metal = false;
+    double sc_fuzz = 0;
+    v3 sc_nrm = mk(0, 0, 0);
     uint64_t rays = 0, nsamples = 0;
     Prof<kProf> pr;
     uint64_t cyc_refill = 0, cyc_walk = 0, cyc_shade = 0;  // wave-uniform (kProf only)
@@ -471,9 +475,15 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
         }
 
         // ---- trace one ray segment per active lane (rayColor's loop body, camera.zig:153-177) --
-        if (active) {
-            bool done;
-            v3 col = mk(0, 0, 0);
+        // Lambertian and Metal scatters each draw exactly one Vec.randomUnitVec and nothing else.
+        // Its rejection loop runs for a geometric number of trips per lane (mean 1.91), but a wave
+        // pays the maximum over its lanes (~6).  So the loop is capped at kRuvTrips trips per
+        // iteration: a lane whose candidates were all rejected stays `pending`, skips the next
+        // walk and continues drawing where it stopped.  Every lane still consumes its own stream
+        // in the reference's order, so the bits do not change.
+        bool done = false;
+        v3 col = mk(0, 0, 0);
+        if (active && !pending) {
             if (bounce >= p.bounce_max) {
                 done = true;  // too many bounces -> black (camera.zig:181)
             } else {
@@ -495,26 +505,17 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
                     const v3 outward = muls(pt - mk(sg.cx, sg.cy, sg.cz), m.inv_r);
                     const bool front = dot(r.dir, outward) < 0;
                     const v3 nrm = front ? outward : -outward;
-                    const v3 albedo = mk(m.albedo[0], m.albedo[1], m.albedo[2]);
-                    v3 dir;
-                    done = false;
-                    // Lambertian and Metal each draw exactly one Vec.randomUnitVec and nothing
-                    // else, so one shared rejection loop serves both (one divergent loop per wave
-                    // instead of two) with the same draws in the same order.
-                    v3 ruv = mk(0, 0, 0);
-                    if (m.kind <= 1) ruv = random_unit_vec(g);
-                    if (m.kind == 0) {  // Lambertian.scatter (material.zig:27-39)
-                        dir = nrm + ruv;
-                        if (near_zero(dir)) dir = nrm;
-                        att = att * albedo;
-                    } else if (m.kind == 1) {  // Metal.scatter (material.zig:55-68)
-                        dir = unit(reflect(r.dir, nrm)) + muls(ruv, m.fuzz);
-                        if (!(dot(dir, nrm) > 0)) {
-                            done = true;  // absorbed -> black
-                        } else {
-                            att = att * albedo;
-                        }
-                    } else {  // Dielectric.scatter (material.zig:82-110)
+                    if (m.kind <= 1) {
+                        // Lambertian (material.zig:27-39) / Metal (:55-68): attenuation = albedo.
+                        // A metal ray that ends up absorbed returns black whatever `att` is, so
+                        // the product can be taken now.
+                        att = att * mk(m.albedo[0], m.albedo[1], m.albedo[2]);
+                        pending = true;
+                        sc_metal = m.kind == 1;
+                        sc_fuzz = m.fuzz;
+                        sc_nrm = nrm;
+                        r.orig = pt;
+                    } else {  // Dielectric.scatter (material.zig:82-110), attenuation (1,1,1)
                         const double ri = front ? 1.0 / m.ior : m.ior;
                         const v3 ud = unit(r.dir);
                         const double cos_t = __builtin_fmin(dot(-ud, nrm), 1.0);
@@ -524,27 +525,49 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
                         r0 = r0 * r0;
                         const double approx = r0 + (1 - r0) * zig_pow5(1 - cos_t);
                         // short-circuit `or` (material.zig:94): draw only if refraction is possible
-                        if (cannot || approx > g.uniform()) {
-                            dir = reflect(ud, nrm);
-                        } else {
-                            dir = refract(ud, nrm, ri);
-                        }
-                    }
-                    if (!done) {
+                        const v3 dir = (cannot || approx > g.uniform()) ? reflect(ud, nrm) : refract(ud, nrm, ri);
                         r.orig = pt;
                         r.dir = dir;
                         ++bounce;
                     }
                 }
             }
-            if (done) {
-                double* dst = samples + 3 * slot;
-                dst[0] = col.x;
-                dst[1] = col.y;
-                dst[2] = col.z;
-                ++nsamples;
-                active = false;
+        }
+        // Vec.randomUnitVec (vec.zig:71-80): at most kRuvTrips rejection trips this iteration
+        double ux = 0, uy = 0, uz = 0, uls = 1;
+        bool got = false;
+        for (int trip = 0; trip < kRuvTrips; ++trip) {
+            const bool want = pending && !got;
+            if (__ballot(want) == 0) break;
+            if (want) got = ruv_candidate(g, ux, uy, uz, uls);
+        }
+        if (got) {  // finish the scatter
+            const double l = __builtin_sqrt(uls);
+            const v3 ruv = mk(ux / l, uy / l, uz / l);
+            v3 dir;
+            bool absorbed = false;
+            if (!sc_metal) {
+                dir = sc_nrm + ruv;
+                if (near_zero(dir)) dir = sc_nrm;
+            } else {
+                dir = unit(reflect(r.dir, sc_nrm)) + muls(ruv, sc_fuzz);
+                absorbed = !(dot(dir, sc_nrm) > 0);  // absorbed -> black
             }
+            pending = false;
+            if (absorbed) {
+                done = true;
+            } else {
+                r.dir = dir;
+                ++bounce;
+            }
+        }
+        if (done) {
+            double* dst = samples + 3 * slot;
+            dst[0] = col.x;
+            dst[1] = col.y;
+            dst[2] = col.z;
+            ++nsamples;
+            active = false;
         }
         if constexpr (kProf) {
             // s_memtime is a scalar op: every lane sees the same stamps; lanes that skipped the

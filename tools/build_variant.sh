@@ -6,7 +6,7 @@ ROOT=$(cd "$(dirname "$0")/.." && pwd)
 REV=$1; NAME=$2
 mkdir -p "$ROOT/ab"
 if [ "$REV" = "WORKTREE" ]; then
-  # EXTRA: extra compiler flags for ablation builds (e.g. -DRTZIG_ABLATE_RUV), built out of tree
+  # EXTRA: extra compiler flags for ablation builds (e.g. -DRTZIG_RUV_TRIPS=2), built out of tree
   if [ -n "$EXTRA" ]; then
     B=/tmp/rtab_$NAME; rm -rf "$B"; mkdir -p "$B"
     C="$ROOT/raytracing-with-zig_amd/csrc"
