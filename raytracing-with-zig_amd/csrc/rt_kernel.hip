@@ -298,7 +298,7 @@ struct BvhWalker {
 
         // stack: entry 0 holds kDone (written once per lane at kernel start), entries 1..sp the
         // pushed far children; a pop reads entry sp, so popping the empty stack yields kDone
-        int sp = 0;
+        int32_t* top = stack;  // this lane's stack entry sp (entry i at stack[i * kBlockBvh])
         int32_t cur = 0;  // root
         // while-while (Aila & Laine 2009): every lane advances through internal nodes until it
         // holds a leaf (or is done); then the lanes with a leaf test its spheres together, so the
@@ -307,7 +307,6 @@ struct BvhWalker {
             while (cur >= 0) {
                 pr.visit();
                 pr.inner_iter();
-                int32_t* top = stack + sp * kBlockBvh;
                 f2 bx0, by0, bz0, bx1, by1, bz1;
                 int32_t ref0, ref1, popped;
                 if constexpr (kLdsNodes) {
@@ -350,7 +349,7 @@ struct BvhWalker {
                 top[kBlockBvh] = first0 ? ref1 : ref0;
                 const bool pick0 = h0 && (!h1 || first0);  // both: nearer; one: that one
                 cur = (h0 || h1) ? (pick0 ? ref0 : ref1) : popped;
-                sp = sp + (int)(h0 && h1) - (int)!(h0 || h1);
+                top += (h0 && h1) ? kBlockBvh : ((h0 || h1) ? 0 : -kBlockBvh);
             }
             if (cur != kDone) {
                 pr.leaf_iter();
@@ -375,8 +374,8 @@ struct BvhWalker {
                 pr.tests(kLeafBvh);
                 upper = (float)closest;
                 upper = upper + __builtin_fabsf(upper) * 0x1p-20f;
-                cur = stack[sp * kBlockBvh];  // pop (entry 0: kDone)
-                --sp;
+                cur = *top;  // pop (entry 0: kDone)
+                top -= kBlockBvh;
             }
         }
         *t_hit = closest;
@@ -413,7 +412,7 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
     // pending Lambertian/Metal scatter (waiting for its randomUnitVec), see below
     bool pending = false, sc_metal = false;
     double sc_fuzz = 0;
-    v3 sc_nrm = mk(0, 0, 0);
+    v3 sc_nrm = mk(0, 0, 0), sc_refl = mk(0, 0, 0);
     uint64_t rays = 0, nsamples = 0;
     Prof<kProf> pr;
     uint64_t cyc_refill = 0, cyc_walk = 0, cyc_shade = 0;  // wave-uniform (kProf only)
@@ -491,45 +490,57 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
                 ++rays;
                 const int k = walk(r, p.t_min, p.t_max, &t, pr);
                 if constexpr (kProf) t_walk1 = __builtin_amdgcn_s_memtime();
+                // Three branches below need a unit vector: the sky (unit(ray.dir).y), the
+                // dielectric (unit(ray.dir)) and the metal (unit(reflect(ray.dir, n))).  Each is a
+                // correctly rounded sqrt and division, and a wave executes every branch some lane
+                // takes; so each lane selects its vector first and one unit() serves all three.
+                GeoRec sg{};
+                MatRec m{};
+                v3 pt = mk(0, 0, 0), nrm = mk(0, 0, 0);
+                bool front = false;
+                v3 x = r.dir;
+                if (k >= 0) {
+                    sg = geo_orig[k];
+                    m = mat_g[k];
+                    // hit record (sphere.zig:44-53)
+                    pt = r.orig + muls(r.dir, t);
+                    const v3 outward = muls(pt - mk(sg.cx, sg.cy, sg.cz), m.inv_r);
+                    front = dot(r.dir, outward) < 0;
+                    nrm = front ? outward : -outward;
+                    if (m.kind == 1) x = reflect(r.dir, nrm);
+                }
+                const v3 u = unit(x);
                 if (k < 0) {
                     // sky gradient (camera.zig:171-177)
-                    const double a = 0.5 * (unit(r.dir).y + 1.0);
+                    const double a = 0.5 * (u.y + 1.0);
                     const v3 sky = muls(mk(1, 1, 1), 1.0 - a) + muls(mk(0.5, 0.7, 1), a);
                     col = att * sky;
                     done = true;
-                } else {
-                    const GeoRec sg = geo_orig[k];
-                    const MatRec m = mat_g[k];
-                    // hit record (sphere.zig:44-53)
-                    const v3 pt = r.orig + muls(r.dir, t);
-                    const v3 outward = muls(pt - mk(sg.cx, sg.cy, sg.cz), m.inv_r);
-                    const bool front = dot(r.dir, outward) < 0;
-                    const v3 nrm = front ? outward : -outward;
-                    if (m.kind <= 1) {
-                        // Lambertian (material.zig:27-39) / Metal (:55-68): attenuation = albedo.
-                        // A metal ray that ends up absorbed returns black whatever `att` is, so
-                        // the product can be taken now.
-                        att = att * mk(m.albedo[0], m.albedo[1], m.albedo[2]);
-                        pending = true;
-                        sc_metal = m.kind == 1;
-                        sc_fuzz = m.fuzz;
-                        sc_nrm = nrm;
-                        r.orig = pt;
-                    } else {  // Dielectric.scatter (material.zig:82-110), attenuation (1,1,1)
-                        const double ri = front ? 1.0 / m.ior : m.ior;
-                        const v3 ud = unit(r.dir);
-                        const double cos_t = __builtin_fmin(dot(-ud, nrm), 1.0);
-                        const double sin_t = __builtin_sqrt(1.0 - cos_t * cos_t);
-                        const bool cannot = ri * sin_t > 1.0;
-                        double r0 = (1 - ri) / (1 + ri);
-                        r0 = r0 * r0;
-                        const double approx = r0 + (1 - r0) * zig_pow5(1 - cos_t);
-                        // short-circuit `or` (material.zig:94): draw only if refraction is possible
-                        const v3 dir = (cannot || approx > g.uniform()) ? reflect(ud, nrm) : refract(ud, nrm, ri);
-                        r.orig = pt;
-                        r.dir = dir;
-                        ++bounce;
-                    }
+                } else if (m.kind <= 1) {
+                    // Lambertian (material.zig:27-39) / Metal (:55-68): attenuation = albedo.  A
+                    // metal ray that ends up absorbed returns black whatever `att` is, so the
+                    // product can be taken now.
+                    att = att * mk(m.albedo[0], m.albedo[1], m.albedo[2]);
+                    pending = true;
+                    sc_metal = m.kind == 1;
+                    sc_fuzz = m.fuzz;
+                    sc_nrm = nrm;
+                    sc_refl = u;
+                    r.orig = pt;
+                } else {  // Dielectric.scatter (material.zig:82-110), attenuation (1,1,1)
+                    const double ri = front ? 1.0 / m.ior : m.ior;
+                    const v3 ud = u;
+                    const double cos_t = __builtin_fmin(dot(-ud, nrm), 1.0);
+                    const double sin_t = __builtin_sqrt(1.0 - cos_t * cos_t);
+                    const bool cannot = ri * sin_t > 1.0;
+                    double r0 = (1 - ri) / (1 + ri);
+                    r0 = r0 * r0;
+                    const double approx = r0 + (1 - r0) * zig_pow5(1 - cos_t);
+                    // short-circuit `or` (material.zig:94): draw only if refraction is possible
+                    const v3 dir = (cannot || approx > g.uniform()) ? reflect(ud, nrm) : refract(ud, nrm, ri);
+                    r.orig = pt;
+                    r.dir = dir;
+                    ++bounce;
                 }
             }
         }
@@ -550,7 +561,7 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
                 dir = sc_nrm + ruv;
                 if (near_zero(dir)) dir = sc_nrm;
             } else {
-                dir = unit(reflect(r.dir, sc_nrm)) + muls(ruv, sc_fuzz);
+                dir = sc_refl + muls(ruv, sc_fuzz);  // unit(reflect(ray.dir, n)) + fuzz * ruv
                 absorbed = !(dot(dir, sc_nrm) > 0);  // absorbed -> black
             }
             pending = false;
