@@ -51,6 +51,23 @@ __device__ __forceinline__ v3 refract(v3 v, v3 n, double eta) {
 // partition of the image over lanes/GPUs draws the same numbers.
 // ------------------------------------------------------------------------------------------------
 __device__ __forceinline__ uint64_t rotl64(uint64_t x, int k) { return (x << k) | (x >> (64 - k)); }
+// rotl64 by a constant K as two v_alignbit_b32 (the compiler's form is a 64-bit shift, a 32-bit
+// shift and an or): for K < 32 the high word is alignbit(hi, lo, 32 - K), the low word
+// alignbit(lo, hi, 32 - K); K >= 32 swaps the words first.
+template <int K>
+__device__ __forceinline__ uint64_t rotl64c(uint64_t x) {
+    static_assert(K > 0 && K < 64 && K != 32, "rotate");
+    uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+    if constexpr (K > 32) {
+        const uint32_t t = lo;
+        lo = hi;
+        hi = t;
+    }
+    constexpr uint32_t s = 32u - (uint32_t)(K & 31);
+    const uint32_t nhi = __builtin_amdgcn_alignbit(hi, lo, s);
+    const uint32_t nlo = __builtin_amdgcn_alignbit(lo, hi, s);
+    return ((uint64_t)nhi << 32) | nlo;
+}
 
 // SplitMix64.next (zig std/Random/SplitMix64.zig)
 __device__ __forceinline__ uint64_t splitmix_next(uint64_t& s) {
@@ -85,26 +102,29 @@ struct Rng {
     }
     // Xoshiro256.next
     __device__ __forceinline__ uint64_t next() {
-        const uint64_t r = rotl64(s0 + s3, 23) + s0;
+        const uint64_t r = rotl64c<23>(s0 + s3) + s0;
         const uint64_t t = s1 << 17;
         s2 ^= s0;
         s3 ^= s1;
         s1 ^= s2;
         s0 ^= s3;
         s2 ^= t;
-        s3 = rotl64(s3, 45);
+        s3 = rotl64c<45>(s3);
         return r;
     }
     // Random.float(f64) (zig std/Random.zig): mantissa = low 52 bits, exponent from leading zeros;
     // >= 12 leading zeros (p = 1/4096) pulls further draws.
     // Fast path on 32-bit halves: fewer than 12 leading zeros <=> hi >= 2^20, and then the leading
-    // one lies in hi, so lz = clz(hi) and the high word of the result is bfi(0xfffff, hi, e << 20).
+    // one lies in hi, so lz = clz(hi) and the high word of the result is (hi & 0xfffff) | e << 20.
     __device__ __forceinline__ double uniform() {
         const uint64_t rnd = next();
         const uint32_t hi = (uint32_t)(rnd >> 32);
         if (__builtin_expect(hi < (1u << 20), 0)) return uniform_slow(rnd);
-        const uint32_t e = 1022u - (uint32_t)__builtin_clz(hi);
-        const uint32_t ohi = (e << 20) | (hi & 0xfffffu);
+        // ohi = (hi & 0xfffff) | (1022 - lz) << 20 = ((hi & 0xfffff) | 1022 << 20) - lz * 2^20:
+        // v_and_or_b32 + v_mad_i32_i24 (lz <= 11; -2^20 is a valid signed 24-bit factor)
+        const uint32_t t = (hi & 0xfffffu) | (1022u << 20);
+        uint32_t ohi;
+        asm("v_mad_i32_i24 %0, %1, %2, %3" : "=v"(ohi) : "v"((uint32_t)__builtin_clz(hi)), "s"(-(1 << 20)), "v"(t));
         return __builtin_bit_cast(double, ((uint64_t)ohi << 32) | (uint32_t)rnd);
     }
     __device__ __forceinline__ double uniform_slow(uint64_t rnd) {  // p = 2^-12 per draw
