@@ -166,6 +166,13 @@ int rt_color_to_rgb8(const double* linear, size_t n_pixels, uint32_t pixel_strid
 size_t rt_ppm_p6_size(uint32_t width, uint32_t height);
 int rt_ppm_encode_p6(const uint8_t* rgb, uint32_t width, uint32_t height, uint8_t* buf, size_t cap);
 int rt_ppm_save_p6(const char* path, const uint8_t* rgb, uint32_t width, uint32_t height);
+/* PPM.save ASCII byte stream (ppm.zig:25-39, Color.format color.zig:82-87 -> RGB.format :13-18):
+ * "P3\nW H\n255\n" then one "r g b\n" line per pixel, decimal, no padding.
+ * rt_ppm_p3_size gives the exact byte count for these pixels; rt_ppm_encode_p3 writes the stream
+ * into `buf` (cap >= that size). */
+size_t rt_ppm_p3_size(const uint8_t* rgb, uint32_t width, uint32_t height);
+int rt_ppm_encode_p3(const uint8_t* rgb, uint32_t width, uint32_t height, uint8_t* buf, size_t cap);
+int rt_ppm_save_p3(const char* path, const uint8_t* rgb, uint32_t width, uint32_t height);
 
 /* Per-(pixel, sample) stream key (DESIGN.md "RNG"); exposed so host tools can reproduce it. */
 uint64_t rt_sample_key(uint64_t seed, uint64_t pixel, uint64_t sample);

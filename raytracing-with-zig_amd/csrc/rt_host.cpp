@@ -271,6 +271,11 @@ int PPM::saveBinary(const std::string& path) const {
     return rt_ppm_save_p6(path.c_str(), rgb.data(), width, height);
 }
 
+int PPM::save(const std::string& path) const {
+    const auto rgb = toRgb();
+    return rt_ppm_save_p3(path.c_str(), rgb.data(), width, height);
+}
+
 }  // namespace rtzig
 
 // =================================================================================================
@@ -389,6 +394,67 @@ int rt_ppm_save_p6(const char* path, const uint8_t* rgb, uint32_t width, uint32_
     if (!f) { rt_set_last_error(std::string("rt_ppm_save_p6: cannot open ") + path); return RT_ERR_IO; }
     f.write((const char*)buf.data(), (std::streamsize)buf.size());
     if (!f) { rt_set_last_error(std::string("rt_ppm_save_p6: write failed ") + path); return RT_ERR_IO; }
+    return RT_OK;
+}
+
+namespace {
+// decimal digits of a byte value (RGB.format prints "{d}")
+inline size_t dec_len(uint8_t v) { return v >= 100 ? 3 : (v >= 10 ? 2 : 1); }
+inline uint8_t* put_dec(uint8_t* o, uint8_t v) {
+    if (v >= 100) *o++ = (uint8_t)('0' + v / 100);
+    if (v >= 10) *o++ = (uint8_t)('0' + v / 10 % 10);
+    *o++ = (uint8_t)('0' + v % 10);
+    return o;
+}
+}  // namespace
+
+size_t rt_ppm_p3_size(const uint8_t* rgb, uint32_t width, uint32_t height) {
+    char hdr[64];
+    const int hl = std::snprintf(hdr, sizeof hdr, "P3\n%u %u\n255\n", width, height);
+    const size_t n = (size_t)width * height;
+    size_t total = (size_t)hl;
+    if (!rgb) return n ? 0 : total;
+    for (size_t k = 0; k < n; k++)  // "r g b\n"
+        total += dec_len(rgb[3 * k]) + dec_len(rgb[3 * k + 1]) + dec_len(rgb[3 * k + 2]) + 3;
+    return total;
+}
+
+int rt_ppm_encode_p3(const uint8_t* rgb, uint32_t width, uint32_t height, uint8_t* buf, size_t cap) {
+    const size_t n = (size_t)width * height;
+    if (!buf || (!rgb && n)) {
+        rt_set_last_error("rt_ppm_encode_p3: null argument");
+        return RT_ERR_INVALID;
+    }
+    const size_t total = rt_ppm_p3_size(rgb, width, height);
+    if (cap < total) {
+        rt_set_last_error("rt_ppm_encode_p3: buffer too small");
+        return RT_ERR_INVALID;
+    }
+    char hdr[64];
+    const int hl = std::snprintf(hdr, sizeof hdr, "P3\n%u %u\n255\n", width, height);
+    std::memcpy(buf, hdr, (size_t)hl);
+    uint8_t* o = buf + hl;
+    for (size_t k = 0; k < n; k++) {
+        o = put_dec(o, rgb[3 * k]);
+        *o++ = ' ';
+        o = put_dec(o, rgb[3 * k + 1]);
+        *o++ = ' ';
+        o = put_dec(o, rgb[3 * k + 2]);
+        *o++ = '\n';
+    }
+    return RT_OK;
+}
+
+int rt_ppm_save_p3(const char* path, const uint8_t* rgb, uint32_t width, uint32_t height) {
+    if (!path) { rt_set_last_error("rt_ppm_save_p3: null path"); return RT_ERR_INVALID; }
+    if (!rgb && (size_t)width * height) { rt_set_last_error("rt_ppm_save_p3: null pixels"); return RT_ERR_INVALID; }
+    std::vector<uint8_t> buf(rt_ppm_p3_size(rgb, width, height));
+    int rc = rt_ppm_encode_p3(rgb, width, height, buf.data(), buf.size());
+    if (rc) return rc;
+    std::ofstream f(path, std::ios::binary);
+    if (!f) { rt_set_last_error(std::string("rt_ppm_save_p3: cannot open ") + path); return RT_ERR_IO; }
+    f.write((const char*)buf.data(), (std::streamsize)buf.size());
+    if (!f) { rt_set_last_error(std::string("rt_ppm_save_p3: write failed ") + path); return RT_ERR_IO; }
     return RT_OK;
 }
 

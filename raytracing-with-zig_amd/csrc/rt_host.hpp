@@ -8,6 +8,7 @@
 //         .setVUp(..).build()                                       camera.zig:109-345
 //   Camera::render()  -> rt_render on the GPU, then PPM::saveBinary camera.zig:123-145
 //   PPM::saveBinary(path)                                           ppm.zig:42-60
+//   PPM::save(path)                                                 ppm.zig:25-39
 // Only host code lives here: the hot path is the HIP kernel behind rt_render().
 #pragma once
 
@@ -101,6 +102,7 @@ struct PPM {  // ppm.zig:5-61
     std::vector<uint8_t> toRgb() const;              // Color.toRgb per pixel (color.zig:63)
     std::vector<uint8_t> encodeBinary() const;       // saveBinary byte stream
     int saveBinary(const std::string& path) const;   // ppm.zig:42-60
+    int save(const std::string& path) const;         // ppm.zig:25-39 (P3 ASCII)
 };
 
 class Camera {  // camera.zig:82-216

@@ -226,7 +226,7 @@ class DeviceRenderer:
 
 
 class PPM:
-    """ppm.zig:5-61: framebuffer + P6 writer."""
+    """ppm.zig:5-61: framebuffer + P6 (saveBinary) and P3 (save) writers."""
 
     def __init__(self, width, height, pixels):
         self.width, self.height, self.pixels = width, height, pixels
@@ -242,6 +242,15 @@ class PPM:
     def saveBinary(self, path):
         rgb = np.ascontiguousarray(self.toRgb())
         check("rt_ppm_save_p6", load().rt_ppm_save_p6(
+            path.encode(), rgb.ctypes.data_as(C.POINTER(C.c_uint8)), self.width, self.height))
+
+    def encode(self):
+        return encode_p3(self.toRgb(), self.width, self.height)
+
+    def save(self, path):
+        """PPM.save (ppm.zig:25-39): the P3 ASCII file."""
+        rgb = np.ascontiguousarray(self.toRgb())
+        check("rt_ppm_save_p3", load().rt_ppm_save_p3(
             path.encode(), rgb.ctypes.data_as(C.POINTER(C.c_uint8)), self.width, self.height))
 
 
@@ -262,6 +271,16 @@ def encode_p6(rgb, width, height):
     buf = (C.c_uint8 * size)()
     check("rt_ppm_encode_p6", lib.rt_ppm_encode_p6(rgb.ctypes.data_as(C.POINTER(C.c_uint8)),
                                                    width, height, buf, size))
+    return bytes(buf)
+
+
+def encode_p3(rgb, width, height):
+    lib = load()
+    rgb = np.ascontiguousarray(rgb, dtype=np.uint8)
+    ptr = rgb.ctypes.data_as(C.POINTER(C.c_uint8))
+    size = lib.rt_ppm_p3_size(ptr, width, height)
+    buf = (C.c_uint8 * size)()
+    check("rt_ppm_encode_p3", lib.rt_ppm_encode_p3(ptr, width, height, buf, size))
     return bytes(buf)
 
 

@@ -29,6 +29,9 @@ EXPORTED = [
     "rt_ppm_p6_size",
     "rt_ppm_encode_p6",
     "rt_ppm_save_p6",
+    "rt_ppm_p3_size",
+    "rt_ppm_encode_p3",
+    "rt_ppm_save_p3",
     "rt_sample_key",
     "rt_last_error",
     "rt_abi_version",
@@ -67,6 +70,10 @@ def _declare(lib):
         "rt_ppm_encode_p6": (C.c_int, [P(C.c_uint8), C.c_uint32, C.c_uint32, P(C.c_uint8),
                                        C.c_size_t]),
         "rt_ppm_save_p6": (C.c_int, [C.c_char_p, P(C.c_uint8), C.c_uint32, C.c_uint32]),
+        "rt_ppm_p3_size": (C.c_size_t, [P(C.c_uint8), C.c_uint32, C.c_uint32]),
+        "rt_ppm_encode_p3": (C.c_int, [P(C.c_uint8), C.c_uint32, C.c_uint32, P(C.c_uint8),
+                                       C.c_size_t]),
+        "rt_ppm_save_p3": (C.c_int, [C.c_char_p, P(C.c_uint8), C.c_uint32, C.c_uint32]),
         "rt_sample_key": (C.c_uint64, [C.c_uint64, C.c_uint64, C.c_uint64]),
         "rt_last_error": (C.c_char_p, []),
         "rt_abi_version": (C.c_int, []),

@@ -102,3 +102,40 @@ def test_scene_add_clamps_radius():
     """Sphere.init clamps the radius to >= 0 (sphere.zig:21)."""
     s = rtzig.Scene.init(1).add((0, 0, 0), -3.0, RT_LAMBERTIAN)
     assert s.world[0].radius == 0.0
+
+
+def test_ppm_p3_one_pixel_kat():
+    """ppm.zig:73-90: a 1x1 black image saved as P3."""
+    assert rtzig.encode_p3(np.zeros((1, 1, 3), np.uint8), 1, 1) == b"P3\n1 1\n255\n0 0 0\n"
+
+
+def test_ppm_p3_matches_reference_chapter2(golden_dir):
+    """The P3 writer reproduces the reference's images/chapter2.ppm byte-for-byte from the book's
+    chapter-2 gradient (r = trunc(255.999 i/(W-1)), g = trunc(255.999 j/(H-1)), b = 0)."""
+    W = H = 256
+    i = np.arange(W, dtype=np.float64)[None, :].repeat(H, 0)
+    j = np.arange(H, dtype=np.float64)[:, None].repeat(W, 1)
+    rgb = np.stack([(255.999 * (i / (W - 1))).astype(np.uint8), (255.999 * (j / (H - 1))).astype(np.uint8),
+                    np.zeros((H, W), np.uint8)], axis=-1)
+    ref = open(os.path.join(golden_dir, "chapter2.ppm"), "rb").read()
+    assert rtzig.encode_p3(rgb, W, H) == ref
+
+
+def test_ppm_p3_save_and_consistency_with_p6(tmp_path):
+    """PPM.save writes the P3 stream; its numbers are exactly the P6 payload (same toRgb)."""
+    rng = np.random.default_rng(3)
+    lin = rng.random((7, 5, 3)) * 1.3 - 0.1
+    ppm = rtzig.PPM(5, 7, lin)
+    path = str(tmp_path / "a.ppm")
+    ppm.save(path)
+    data = open(path, "rb").read()
+    assert data == ppm.encode()
+    head, body = data.split(b"\n", 3)[:3], data.split(b"\n", 3)[3]
+    assert head == [b"P3", b"5 7", b"255"]
+    nums = np.array([int(x) for x in body.split()], np.uint8)
+    p6 = ppm.encodeBinary()
+    assert np.array_equal(nums, np.frombuffer(p6[len(b"P6\n5 7\n255\n"):-1], np.uint8))
+    # 0..255 round trip, including 1-, 2- and 3-digit values
+    allv = np.arange(256, dtype=np.uint8).repeat(3).reshape(16, 16, 3)
+    txt = rtzig.encode_p3(allv, 16, 16)
+    assert [int(x) for x in txt.split()[4:]] == list(allv.reshape(-1))
