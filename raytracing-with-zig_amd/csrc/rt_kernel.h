@@ -32,6 +32,10 @@ struct alignas(16) MatRec {
     double fuzz;
     double ior;
     double inv_r;   // 1.0 / radius, as Vec.divScalar computes it (vec.zig:44, sphere.zig:45)
+    // Dielectric constants, computed on the host with the device's IEEE operations (same bits):
+    double inv_ior;   // 1.0 / ior: ri of a front-face hit (material.zig:86)
+    double r0_front;  // Schlick r0 = ((1 - ri) / (1 + ri))^2 for ri = inv_ior (material.zig:106-108)
+    double r0_back;   // ... for ri = ior
     uint32_t kind;  // 0 lambertian, 1 metal, 2 dielectric
     uint32_t pad;
 };
@@ -69,6 +73,9 @@ constexpr int kBlockBvh = 512;     // 8 waves; 2 blocks per CU share the LDS bud
 constexpr int kMaxDepthBvh = 16;   // == rtbvh::kMaxDepth: bound on per-lane LDS stack entries (entry 0: "done")
 #ifndef RTZIG_LEAF
 #define RTZIG_LEAF 2
+#endif
+#ifndef RTZIG_LEAF_FILTER
+#define RTZIG_LEAF_FILTER 1  // 0: every slot with disc >= 0; 1: drop spheres behind; 2: also beyond closest
 #endif
 constexpr int kLeafBvh = RTZIG_LEAF;       // == rtbvh::kLeafMax: slots per (sentinel-padded) leaf
 struct alignas(8) BvhNode {

@@ -133,6 +133,27 @@ __device__ __forceinline__ int world_hit(const GeoRec* __restrict__ geo, uint32_
     return best;
 }
 
+// x / l for several numerators x sharing one denominator l, bit-identical to the compiler's
+// correctly rounded f64 division (v_div_scale, v_rcp_f64, two Newton steps, q0 = x*y,
+// r = fma(-l, q0, x), v_div_fmas = fma(r, y, q0), v_div_fixup) whenever that sequence does not
+// scale: the reciprocal part depends on l alone, so it is computed once.  Valid (no scaling, no
+// fixup) for l in [2^-300, 1] and |x| in {0} U [2^-53, l]; Vec.randomUnitVec (vec.zig:71-80)
+// guarantees both: |p|^2 in (1e-160, 1], so l in (1e-80, 1]; each component is -1 + 2u with u a
+// Random.float(f64) (granularity <= 2^-54 below 0.5), so it is 0 or at least 2^-53 in magnitude,
+// and |x| <= l.  x == 0 gives +0 both ways (fixup of 0 / l).
+struct SharedRcp {
+    double l, y;
+    __device__ __forceinline__ explicit SharedRcp(double den) : l(den) {
+        const double y0 = __builtin_amdgcn_rcp(den);
+        const double y1 = __builtin_fma(y0, __builtin_fma(-den, y0, 1.0), y0);
+        y = __builtin_fma(y1, __builtin_fma(-den, y1, 1.0), y1);
+    }
+    __device__ __forceinline__ double div(double x) const {
+        const double q0 = x * y;
+        return __builtin_fma(__builtin_fma(-l, q0, x), y, q0);
+    }
+};
+
 __device__ __forceinline__ uint32_t lane_id() {
     return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
 }
@@ -152,11 +173,14 @@ struct Prof {
     __device__ __forceinline__ void visit() {}
     __device__ __forceinline__ void inner_iter() {}
     __device__ __forceinline__ void leaf_iter() {}
+    __device__ __forceinline__ void cand_block() {}
+    __device__ __forceinline__ void root2_block() {}
 };
 template <>
 struct Prof<true> {
     uint64_t n_tests = 0, n_visits = 0;
     uint64_t w_inner = 0, w_leaf = 0;  // wave-level iterations (counted by the first active lane)
+    uint64_t w_cand = 0, w_root2 = 0;  // wave-level candidate blocks (sqrt + root1 division) / root2 divisions
     __device__ __forceinline__ void tests(uint32_t n) { n_tests += n; }
     __device__ __forceinline__ void visit() { ++n_visits; }
     __device__ __forceinline__ static bool leader() {
@@ -165,6 +189,8 @@ struct Prof<true> {
     }
     __device__ __forceinline__ void inner_iter() { w_inner += leader() ? 1 : 0; }
     __device__ __forceinline__ void leaf_iter() { w_leaf += leader() ? 1 : 0; }
+    __device__ __forceinline__ void cand_block() { w_cand += leader() ? 1 : 0; }
+    __device__ __forceinline__ void root2_block() { w_root2 += leader() ? 1 : 0; }
 };
 
 // ------------------------------------------------------------------------------------------------
@@ -224,6 +250,44 @@ __device__ __forceinline__ uint32_t lds_addr(const void* p) {
     return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
 }
 
+// Exact candidate filters for the leaf round (RTZIG_LEAF_FILTER >= 1).  With s = fl(sqrt(disc)),
+// the reference's roots are root1 = fl(fl(h - s) / a) <= root2 = fl(fl(h + s) / a), and the
+// candidate of a sphere is root1 if t_min < root1, else root2 if t_min < root2 (sphere.zig:35-41).
+//   behind(h, disc):            proves root2 <= t_min, so the sphere yields no candidate;
+//   beyond(h, disc, closest):   proves root1 > closest, so its candidate (>= root1) cannot win, not
+//                               even by the lower-index tie rule.
+// Both are evaluated with explicit fma and margins of 2^-30 relative (plus a * 2^-600 absolute)
+// that dominate every rounding error of the comparison (a few ulps), so neither ever rejects a
+// sphere the exact candidate() would accept; NaN or inf operands make the tests false (keep the
+// sphere).  Proof for behind (beyond is symmetric): Z = (t_min*a - margins) - h - 2^-30|h|;
+// Z > 0 and Z*Z > disc*(1 + 2^-30) give s < Z, hence h + s < t_min*a by more than the rounding of
+// fl(h + s), so fl(h + s) / a < t_min and root1 <= root2 <= t_min.  The filters need a within
+// [2^-400, 2^400] (else they never reject).  Typical catch: the sphere a secondary ray starts on
+// (c ~ 0, h < 0), whose candidate otherwise costs a sqrt and two divisions for the whole wave.
+struct LeafFilter {
+    double a_tiny;  // a * 2^-600 (0 when the filters are off)
+    double tm_lim;  // t_min * a lowered by the margins
+    bool on;
+    __device__ __forceinline__ static LeafFilter make(double a, double t_min) {
+        LeafFilter f;
+        f.on = a > 0x1p-400 && a < 0x1p400;
+        f.a_tiny = a * 0x1p-600;
+        const double pm = t_min * a;
+        f.tm_lim = __builtin_fma(-__builtin_fabs(pm), 0x1p-30, pm) - f.a_tiny;
+        return f;
+    }
+    __device__ __forceinline__ bool behind(double h, double disc) const {
+        const double z = __builtin_fma(-__builtin_fabs(h), 0x1p-30, tm_lim - h);
+        return on && z > 0 && __builtin_fma(z, z, -(disc * (1 + 0x1p-30))) > 0;
+    }
+    __device__ __forceinline__ bool beyond(double h, double disc, double a, double closest) const {
+        const double pc = closest * a;
+        const double tc = __builtin_fma(__builtin_fabs(pc), 0x1p-30, pc) + a_tiny;
+        const double y = __builtin_fma(-__builtin_fabs(h), 0x1p-30, h - tc);
+        return on && y > 0 && __builtin_fma(y, y, -(disc * (1 + 0x1p-30))) > 0;
+    }
+};
+
 template <bool kLdsNodes>
 struct BvhWalker {
     const BvhNode* __restrict__ nodes;
@@ -234,8 +298,9 @@ struct BvhWalker {
     int32_t* stack;                      // LDS, element i of this lane at stack[i * kBlockBvh]
 
     // always-list sphere q
-    __device__ __forceinline__ void test_always(uint32_t q, const Ray& r, double a, double t_min, double& closest,
-                                                uint32_t& best, bool& found) const {
+    template <class PR>
+    __device__ __forceinline__ void test_always(uint32_t q, const Ray& r, double a, double t_min, const LeafFilter& lfilt,
+                                                double& closest, uint32_t& best, bool& found, PR& pr) const {
         const GeoRec s = ageo[q];
         const double ocx = s.cx - r.orig.x;
         const double ocy = s.cy - r.orig.y;
@@ -243,17 +308,27 @@ struct BvhWalker {
         const double h = (r.dir.x * ocx + r.dir.y * ocy) + r.dir.z * ocz;
         const double c = ((ocx * ocx + ocy * ocy) + ocz * ocz) - s.r2;
         const double disc = h * h - a * c;
-        if (disc >= 0) candidate(asid[q], h, disc, a, t_min, closest, best, found);
+#if RTZIG_LEAF_FILTER == 0
+        if (disc >= 0) candidate(asid[q], h, disc, a, t_min, closest, best, found, pr);
+#else
+        // the ground sphere is "behind" every ray that leaves it: no sqrt / second-root division
+        if (disc >= 0 && !lfilt.behind(h, disc)) candidate(asid[q], h, disc, a, t_min, closest, best, found, pr);
+#endif
     }
 
     // root selection of sphere.zig:35-41 for a sphere with disc >= 0, then the first-wins argmin.
-    // (A branch-free form that computes both roots for every lane measured 4% slower.)
+    // The argmin is order-independent (ties go to the lower original index), so candidates may be
+    // taken in any order.  (A branch-free form that computes both roots for every lane measured 4%
+    // slower.)
+    template <class PR>
     __device__ __forceinline__ static void candidate(uint32_t k, double h, double disc, double a, double t_min,
-                                                     double& closest, uint32_t& best, bool& found) {
+                                                     double& closest, uint32_t& best, bool& found, PR& pr) {
+        pr.cand_block();
         const double sq = __builtin_sqrt(disc);
         double ts = (h - sq) / a;
         bool cand = t_min < ts;
         if (!cand) {
+            pr.root2_block();
             ts = (h + sq) / a;
             cand = t_min < ts;
         }
@@ -270,7 +345,8 @@ struct BvhWalker {
         double closest = t_max;
         uint32_t best = 0;
         bool found = false;
-        for (uint32_t q = 0; q < n_always; ++q) test_always(q, r, a, t_min, closest, best, found);
+        const LeafFilter lfilt = LeafFilter::make(a, t_min);
+        for (uint32_t q = 0; q < n_always; ++q) test_always(q, r, a, t_min, lfilt, closest, best, found, pr);
         pr.tests(n_always);
 
         // f32 ray for the conservative slab tests (error budget: rt_bvh.cpp)
@@ -367,10 +443,55 @@ struct BvhWalker {
                     const double c = ((ocx * ocx + ocy * ocy) + ocz * ocz) - s.r2;
                     disc[u] = h[u] * h[u] - a * c;
                 }
+#if RTZIG_LEAF_FILTER == 0
 #pragma unroll
                 for (int u = 0; u < kLeafBvh; ++u) {
-                    if (disc[u] >= 0) candidate(lf->sid[u], h[u], disc[u], a, t_min, closest, best, found);
+                    if (disc[u] >= 0) candidate(lf->sid[u], h[u], disc[u], a, t_min, closest, best, found, pr);
                 }
+#else
+                // Compacted candidates: a wave pays a candidate block (sqrt + division) whenever ANY
+                // of its lanes needs it, so each lane first drops the slots that provably cannot
+                // win (LeafFilter) and then feeds its viable slots through ONE block per round,
+                // nearest-looking (smallest h) first; a second round runs only for lanes with a
+                // second slot still viable after `closest` has shrunk.
+                bool v[kLeafBvh];
+                uint32_t sid[kLeafBvh];
+#pragma unroll
+                for (int u = 0; u < kLeafBvh; ++u) {
+                    sid[u] = lf->sid[u];
+                    v[u] = disc[u] >= 0 && !lfilt.behind(h[u], disc[u]);
+#if RTZIG_LEAF_FILTER >= 2
+                    v[u] = v[u] && !lfilt.beyond(h[u], disc[u], a, closest);
+#endif
+                }
+#pragma unroll
+                for (int rd = 0; rd < kLeafBvh; ++rd) {
+                    bool any = false;
+                    double hb = 0, db = 0;
+                    uint32_t kb = 0;
+                    int pb = 0;
+#pragma unroll
+                    for (int u = 0; u < kLeafBvh; ++u) {
+                        const bool take = v[u] && (!any || h[u] < hb);
+                        hb = take ? h[u] : hb;
+                        db = take ? disc[u] : db;
+                        kb = take ? sid[u] : kb;
+                        pb = take ? u : pb;
+                        any = any || v[u];
+                    }
+                    if (!any) break;
+                    candidate(kb, hb, db, a, t_min, closest, best, found, pr);
+                    if (rd + 1 < kLeafBvh) {
+#pragma unroll
+                        for (int u = 0; u < kLeafBvh; ++u) {
+                            v[u] = v[u] && u != pb;
+#if RTZIG_LEAF_FILTER >= 2
+                            v[u] = v[u] && !lfilt.beyond(h[u], disc[u], a, closest);
+#endif
+                        }
+                    }
+                }
+#endif
                 pr.tests(kLeafBvh);
                 upper = (float)closest;
                 upper = upper + __builtin_fabsf(upper) * 0x1p-20f;
@@ -528,13 +649,12 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
                     sc_refl = u;
                     r.orig = pt;
                 } else {  // Dielectric.scatter (material.zig:82-110), attenuation (1,1,1)
-                    const double ri = front ? 1.0 / m.ior : m.ior;
+                    const double ri = front ? m.inv_ior : m.ior;  // 1.0 / ior precomputed (same bits)
                     const v3 ud = u;
                     const double cos_t = __builtin_fmin(dot(-ud, nrm), 1.0);
                     const double sin_t = __builtin_sqrt(1.0 - cos_t * cos_t);
                     const bool cannot = ri * sin_t > 1.0;
-                    double r0 = (1 - ri) / (1 + ri);
-                    r0 = r0 * r0;
+                    const double r0 = front ? m.r0_front : m.r0_back;  // ((1-ri)/(1+ri))^2, host
                     const double approx = r0 + (1 - r0) * zig_pow5(1 - cos_t);
                     // short-circuit `or` (material.zig:94): draw only if refraction is possible
                     const v3 dir = (cannot || approx > g.uniform()) ? reflect(ud, nrm) : refract(ud, nrm, ri);
@@ -554,7 +674,8 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
         }
         if (got) {  // finish the scatter
             const double l = __builtin_sqrt(uls);
-            const v3 ruv = mk(ux / l, uy / l, uz / l);
+            const SharedRcp rl(l);
+            const v3 ruv = mk(rl.div(ux), rl.div(uy), rl.div(uz));  // p / sqrt(|p|^2), true divisions
             v3 dir;
             bool absorbed = false;
             if (!sc_metal) {
@@ -614,16 +735,20 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
                 nt += __shfl_xor(nt, off, 64);
                 nv += __shfl_xor(nv, off, 64);
             }
-            uint64_t wi = pr.w_inner, wl = pr.w_leaf;
+            uint64_t wi = pr.w_inner, wl = pr.w_leaf, wc = pr.w_cand, w2 = pr.w_root2;
             for (int off = 32; off > 0; off >>= 1) {
                 wi += __shfl_xor(wi, off, 64);
                 wl += __shfl_xor(wl, off, 64);
+                wc += __shfl_xor(wc, off, 64);
+                w2 += __shfl_xor(w2, off, 64);
             }
             if (lane == 0) {
                 atomicAdd(&stats[2], (unsigned long long)nt);
                 atomicAdd(&stats[3], (unsigned long long)nv);
                 atomicAdd(&stats[7], (unsigned long long)wi);
                 atomicAdd(&stats[8], (unsigned long long)wl);
+                atomicAdd(&stats[9], (unsigned long long)wc);
+                atomicAdd(&stats[10], (unsigned long long)w2);
                 atomicAdd(&stats[4], (unsigned long long)cyc_refill);
                 atomicAdd(&stats[5], (unsigned long long)cyc_walk);
                 atomicAdd(&stats[6], (unsigned long long)cyc_shade);

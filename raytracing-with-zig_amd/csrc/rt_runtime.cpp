@@ -326,6 +326,14 @@ int rt_context_set_scene(rt_context* ctx, const rt_sphere* spheres, size_t n) {
         mat[k].fuzz = spheres[k].fuzz;
         mat[k].ior = spheres[k].refraction_index;
         mat[k].inv_r = 1.0 / r;
+        const double ior = spheres[k].refraction_index;
+        mat[k].inv_ior = 1.0 / ior;
+        for (int face = 0; face < 2; face++) {  // reflectance()'s r0 (material.zig:106-108) per face
+            const double ri = face == 0 ? mat[k].inv_ior : ior;
+            double r0 = (1 - ri) / (1 + ri);
+            r0 = r0 * r0;
+            (face == 0 ? mat[k].r0_front : mat[k].r0_back) = r0;
+        }
         mat[k].kind = spheres[k].material;
     }
     if (n_pad > ctx->capacity) {

@@ -51,6 +51,8 @@ for v in args.variants.split():
         "wave_inner_iters_per_wave_iter": round(s[7] / max(1, s[0] / 64), 3),
         "wave_leaf_rounds_per_wave_iter": round(s[8] / max(1, s[0] / 64), 3),
         "lane_util_inner": round(s[3] / max(1, s[7] * 64), 4),
+        "wave_cand_blocks_per_wave_iter": round(s[9] / max(1, s[0] / 64), 3),
+        "wave_root2_blocks_per_wave_iter": round(s[10] / max(1, s[0] / 64), 3),
         "cycle_split": {"refill": round(s[4] / cyc, 4), "walk": round(s[5] / cyc, 4), "shade": round(s[6] / cyc, 4)},
         "raw": s,
     }
