@@ -69,6 +69,19 @@ __device__ __forceinline__ uint64_t rotl64c(uint64_t x) {
     return ((uint64_t)nhi << 32) | nlo;
 }
 
+// a ^ b ^ c of 64-bit words as two gfx950 v_bitop3_b32 (truth table 0x96 = 3-input parity); the
+// compiler emits two v_xor_b32 per 64-bit xor and does not form this on its own.
+__device__ __forceinline__ uint32_t xor3_32(uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t r;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+__device__ __forceinline__ uint64_t xor3_64(uint64_t a, uint64_t b, uint64_t c) {
+    const uint32_t lo = xor3_32((uint32_t)a, (uint32_t)b, (uint32_t)c);
+    const uint32_t hi = xor3_32((uint32_t)(a >> 32), (uint32_t)(b >> 32), (uint32_t)(c >> 32));
+    return ((uint64_t)hi << 32) | lo;
+}
+
 // SplitMix64.next (zig std/Random/SplitMix64.zig)
 __device__ __forceinline__ uint64_t splitmix_next(uint64_t& s) {
     s += 0x9e3779b97f4a7c15ULL;
@@ -100,16 +113,20 @@ struct Rng {
         s2 = splitmix_next(sm);
         s3 = splitmix_next(sm);
     }
-    // Xoshiro256.next
+    // Xoshiro256.next: s2 ^= s0; s3 ^= s1; s1 ^= s2; s0 ^= s3; s2 ^= t; s3 = rotl(s3, 45), with the
+    // chained xors folded into 3-input ones (s1 ^ s2 ^ s0, s0 ^ s3 ^ s1, s2 ^ s0 ^ t): 8 bitwise
+    // ops per draw instead of 12
     __device__ __forceinline__ uint64_t next() {
         const uint64_t r = rotl64c<23>(s0 + s3) + s0;
         const uint64_t t = s1 << 17;
-        s2 ^= s0;
-        s3 ^= s1;
-        s1 ^= s2;
-        s0 ^= s3;
-        s2 ^= t;
-        s3 = rotl64c<45>(s3);
+        const uint64_t n1 = xor3_64(s1, s2, s0);
+        const uint64_t n0 = xor3_64(s0, s3, s1);
+        const uint64_t n2 = xor3_64(s2, s0, t);
+        const uint64_t n3 = s3 ^ s1;
+        s0 = n0;
+        s1 = n1;
+        s2 = n2;
+        s3 = rotl64c<45>(n3);
         return r;
     }
     // Random.float(f64) (zig std/Random.zig): mantissa = low 52 bits, exponent from leading zeros;

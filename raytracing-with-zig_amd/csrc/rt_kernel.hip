@@ -141,6 +141,20 @@ __device__ __forceinline__ int world_hit(const GeoRec* __restrict__ geo, uint32_
 // guarantees both: |p|^2 in (1e-160, 1], so l in (1e-80, 1]; each component is -1 + 2u with u a
 // Random.float(f64) (granularity <= 2^-54 below 0.5), so it is 0 or at least 2^-53 in magnitude,
 // and |x| <= l.  x == 0 gives +0 both ways (fixup of 0 / l).
+// sqrt(x) bit-identical to the compiler's correctly rounded f64 sqrt for x in [2^-767, 2^1023]:
+// that sequence scales x by 2^256 only below 2^-767 and patches only +-0 / +inf / NaN
+// (v_cmp_class); in between both are identity, and what remains is this rsq + Newton sequence.
+__device__ __forceinline__ double sqrt_normal(double x) {
+    const double y = __builtin_amdgcn_rsq(x);
+    double g = x * y;
+    double h = y * 0.5;
+    const double r = __builtin_fma(-h, g, 0.5);
+    g = __builtin_fma(g, r, g);
+    h = __builtin_fma(h, r, h);
+    g = __builtin_fma(__builtin_fma(-g, g, x), h, g);
+    return __builtin_fma(__builtin_fma(-g, g, x), h, g);
+}
+
 struct SharedRcp {
     double l, y;
     __device__ __forceinline__ explicit SharedRcp(double den) : l(den) {
@@ -673,7 +687,7 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
             if (want) got = ruv_candidate(g, ux, uy, uz, uls);
         }
         if (got) {  // finish the scatter
-            const double l = __builtin_sqrt(uls);
+            const double l = sqrt_normal(uls);  // |p|^2 in (1e-160, 1] (vec.zig:76)
             const SharedRcp rl(l);
             const v3 ruv = mk(rl.div(ux), rl.div(uy), rl.div(uz));  // p / sqrt(|p|^2), true divisions
             v3 dir;
