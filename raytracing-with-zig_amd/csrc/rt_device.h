@@ -30,8 +30,60 @@ __device__ __forceinline__ v3 muls(v3 a, double s) { return v3{a.x * s, a.y * s,
 // Vec.dot / lenSquared: @reduce(.Add) is the ordered (x+y)+z (vec.zig:51,114)
 __device__ __forceinline__ double dot(v3 a, v3 b) { return (a.x * b.x + a.y * b.y) + a.z * b.z; }
 __device__ __forceinline__ double len_sq(v3 a) { return (a.x * a.x + a.y * a.y) + a.z * a.z; }
-// Vec.unit = divScalar(v, len) = v * (1/len) (vec.zig:39-45,126)
-__device__ __forceinline__ v3 unit(v3 a) { return muls(a, 1.0 / __builtin_sqrt(len_sq(a))); }
+// sqrt(x) bit-identical to the compiler's correctly rounded f64 sqrt for x in [2^-767, 2^1023]:
+// that sequence scales x by 2^256 only below 2^-767 and patches only +-0 / +inf / NaN
+// (v_cmp_class); in between both are identity, and what remains is this rsq + Newton sequence.
+__device__ __forceinline__ double sqrt_normal(double x) {
+    const double y = __builtin_amdgcn_rsq(x);
+    double g = x * y;
+    double h = y * 0.5;
+    const double r = __builtin_fma(-h, g, 0.5);
+    g = __builtin_fma(g, r, g);
+    h = __builtin_fma(h, r, h);
+    g = __builtin_fma(__builtin_fma(-g, g, x), h, g);
+    return __builtin_fma(__builtin_fma(-g, g, x), h, g);
+}
+
+struct SharedRcp {
+    double l, y;
+    __device__ __forceinline__ explicit SharedRcp(double den) : l(den) {
+        const double y0 = __builtin_amdgcn_rcp(den);
+        const double y1 = __builtin_fma(y0, __builtin_fma(-den, y0, 1.0), y0);
+        y = __builtin_fma(y1, __builtin_fma(-den, y1, 1.0), y1);
+    }
+    __device__ __forceinline__ double div(double x) const {
+        const double q0 = x * y;
+        return __builtin_fma(__builtin_fma(-l, q0, x), y, q0);
+    }
+};
+
+// __builtin_sqrt(x) with the unscaled sequence when x is in [2^-767, inf) (the high word minus
+// that of 2^-767 is below 0x7ff00000 - 0x10000000 as an unsigned number); other lanes (0, tiny,
+// inf, NaN, negative) take the compiler's full sequence, which a wave skips when none needs it.
+__device__ __forceinline__ bool sqrt_in_range(double x) {
+    return (uint32_t)(__builtin_bit_cast(uint64_t, x) >> 32) - 0x10000000u < 0x6ff00000u;
+}
+__device__ __forceinline__ double sqrt_g(double x) {
+    if (__builtin_expect(sqrt_in_range(x), 1)) return sqrt_normal(x);
+    return __builtin_sqrt(x);
+}
+
+// Vec.unit = divScalar(v, len) = v * (1/len) (vec.zig:39-45,126).  For |v|^2 in [2^-767, inf),
+// len is in [2^-384, 2^512]: 1/len needs no scaling, so it is the Newton reciprocal of SharedRcp
+// followed by the division's last two steps with numerator 1 (q0 = y, r = fma(-len, y, 1),
+// q = fma(r, y, y)) — the same bits as the correctly rounded 1.0 / len.
+__device__ __forceinline__ v3 unit(v3 a) {
+    const double ls = len_sq(a);
+    double inv;
+    if (__builtin_expect(sqrt_in_range(ls), 1)) {
+        const double len = sqrt_normal(ls);
+        const double y = SharedRcp(len).y;
+        inv = __builtin_fma(__builtin_fma(-len, y, 1.0), y, y);
+    } else {
+        inv = 1.0 / __builtin_sqrt(ls);
+    }
+    return muls(a, inv);
+}
 // Vec.nearZero: all(v < 1e-8) with no abs (vec.zig:26-29)
 __device__ __forceinline__ bool near_zero(v3 v) { return v.x < 1e-8 && v.y < 1e-8 && v.z < 1e-8; }
 // Vec.reflect = v - (n * dot(v,n)) * 2 (vec.zig:103-105)
@@ -40,7 +92,7 @@ __device__ __forceinline__ v3 reflect(v3 v, v3 n) { return v - muls(muls(n, dot(
 __device__ __forceinline__ v3 refract(v3 v, v3 n, double eta) {
     const double cos_t = __builtin_fmin(dot(-v, n), 1.0);
     const v3 r_perp = muls(v + muls(n, cos_t), eta);
-    const v3 r_par = muls(n, -__builtin_sqrt(__builtin_fabs(1.0 - len_sq(r_perp))));
+    const v3 r_par = muls(n, -sqrt_g(__builtin_fabs(1.0 - len_sq(r_perp))));
     return r_perp + r_par;
 }
 

@@ -115,7 +115,7 @@ __device__ __forceinline__ int world_hit(const GeoRec* __restrict__ geo, uint32_
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             if (disc[u] >= 0) {  // !(disc < 0); a NaN disc rejects either way
-                const double sq = __builtin_sqrt(disc[u]);
+                const double sq = sqrt_g(disc[u]);
                 double root = (h[u] - sq) / a;
                 bool ok = t_min < root && root < closest;
                 if (!ok) {
@@ -141,33 +141,6 @@ __device__ __forceinline__ int world_hit(const GeoRec* __restrict__ geo, uint32_
 // guarantees both: |p|^2 in (1e-160, 1], so l in (1e-80, 1]; each component is -1 + 2u with u a
 // Random.float(f64) (granularity <= 2^-54 below 0.5), so it is 0 or at least 2^-53 in magnitude,
 // and |x| <= l.  x == 0 gives +0 both ways (fixup of 0 / l).
-// sqrt(x) bit-identical to the compiler's correctly rounded f64 sqrt for x in [2^-767, 2^1023]:
-// that sequence scales x by 2^256 only below 2^-767 and patches only +-0 / +inf / NaN
-// (v_cmp_class); in between both are identity, and what remains is this rsq + Newton sequence.
-__device__ __forceinline__ double sqrt_normal(double x) {
-    const double y = __builtin_amdgcn_rsq(x);
-    double g = x * y;
-    double h = y * 0.5;
-    const double r = __builtin_fma(-h, g, 0.5);
-    g = __builtin_fma(g, r, g);
-    h = __builtin_fma(h, r, h);
-    g = __builtin_fma(__builtin_fma(-g, g, x), h, g);
-    return __builtin_fma(__builtin_fma(-g, g, x), h, g);
-}
-
-struct SharedRcp {
-    double l, y;
-    __device__ __forceinline__ explicit SharedRcp(double den) : l(den) {
-        const double y0 = __builtin_amdgcn_rcp(den);
-        const double y1 = __builtin_fma(y0, __builtin_fma(-den, y0, 1.0), y0);
-        y = __builtin_fma(y1, __builtin_fma(-den, y1, 1.0), y1);
-    }
-    __device__ __forceinline__ double div(double x) const {
-        const double q0 = x * y;
-        return __builtin_fma(__builtin_fma(-l, q0, x), y, q0);
-    }
-};
-
 __device__ __forceinline__ uint32_t lane_id() {
     return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
 }
@@ -338,7 +311,7 @@ struct BvhWalker {
     __device__ __forceinline__ static void candidate(uint32_t k, double h, double disc, double a, double t_min,
                                                      double& closest, uint32_t& best, bool& found, PR& pr) {
         pr.cand_block();
-        const double sq = __builtin_sqrt(disc);
+        const double sq = sqrt_g(disc);
         double ts = (h - sq) / a;
         bool cand = t_min < ts;
         if (!cand) {
@@ -666,7 +639,7 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
                     const double ri = front ? m.inv_ior : m.ior;  // 1.0 / ior precomputed (same bits)
                     const v3 ud = u;
                     const double cos_t = __builtin_fmin(dot(-ud, nrm), 1.0);
-                    const double sin_t = __builtin_sqrt(1.0 - cos_t * cos_t);
+                    const double sin_t = sqrt_g(1.0 - cos_t * cos_t);
                     const bool cannot = ri * sin_t > 1.0;
                     const double r0 = front ? m.r0_front : m.r0_back;  // ((1-ri)/(1+ri))^2, host
                     const double approx = r0 + (1 - r0) * zig_pow5(1 - cos_t);
