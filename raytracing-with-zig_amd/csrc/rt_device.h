@@ -57,6 +57,30 @@ struct SharedRcp {
     }
 };
 
+// x / a for the two roots of every sphere test of one ray (sphere.zig:38-40), a = |dir|^2: the
+// reciprocal part of the division is computed once per ray (SharedRcp); each quotient then takes
+// the division's last three steps, bit-identical to the correctly rounded x / a when no operand
+// needs scaling: a in [2^-100, 2^100] (checked per ray) and |x| in [2^-600, 2^600) (biased
+// exponent in [423, 1623), checked per division on the high word shifted past the sign).  Then
+// the quotient lies in [2^-700, 2^700] and v_div_scale / v_div_fixup are the identity.  Other
+// lanes take the compiler's full division.
+struct RayDiv {
+    double a, y;
+    bool ok;
+    __device__ __forceinline__ explicit RayDiv(double den) : a(den) {
+        ok = den >= 0x1p-100 && den <= 0x1p100;
+        y = SharedRcp(den).y;
+    }
+    __device__ __forceinline__ double div(double x) const {
+        const uint32_t hi2 = (uint32_t)(__builtin_bit_cast(uint64_t, x) >> 32) << 1;
+        if (__builtin_expect(ok && hi2 - (423u << 21) < (1200u << 21), 1)) {
+            const double q0 = x * y;
+            return __builtin_fma(__builtin_fma(-a, q0, x), y, q0);
+        }
+        return x / a;
+    }
+};
+
 // __builtin_sqrt(x) with the unscaled sequence when x is in [2^-767, inf) (the high word minus
 // that of 2^-767 is below 0x7ff00000 - 0x10000000 as an unsigned number); other lanes (0, tiny,
 // inf, NaN, negative) take the compiler's full sequence, which a wave skips when none needs it.

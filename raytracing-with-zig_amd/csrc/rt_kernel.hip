@@ -286,7 +286,7 @@ struct BvhWalker {
 
     // always-list sphere q
     template <class PR>
-    __device__ __forceinline__ void test_always(uint32_t q, const Ray& r, double a, double t_min, const LeafFilter& lfilt,
+    __device__ __forceinline__ void test_always(uint32_t q, const Ray& r, double a, const RayDiv& ad, double t_min, const LeafFilter& lfilt,
                                                 double& closest, uint32_t& best, bool& found, PR& pr) const {
         const GeoRec s = ageo[q];
         const double ocx = s.cx - r.orig.x;
@@ -296,10 +296,10 @@ struct BvhWalker {
         const double c = ((ocx * ocx + ocy * ocy) + ocz * ocz) - s.r2;
         const double disc = h * h - a * c;
 #if RTZIG_LEAF_FILTER == 0
-        if (disc >= 0) candidate(asid[q], h, disc, a, t_min, closest, best, found, pr);
+        if (disc >= 0) candidate(asid[q], h, disc, ad, t_min, closest, best, found, pr);
 #else
         // the ground sphere is "behind" every ray that leaves it: no sqrt / second-root division
-        if (disc >= 0 && !lfilt.behind(h, disc)) candidate(asid[q], h, disc, a, t_min, closest, best, found, pr);
+        if (disc >= 0 && !lfilt.behind(h, disc)) candidate(asid[q], h, disc, ad, t_min, closest, best, found, pr);
 #endif
     }
 
@@ -308,15 +308,15 @@ struct BvhWalker {
     // taken in any order.  (A branch-free form that computes both roots for every lane measured 4%
     // slower.)
     template <class PR>
-    __device__ __forceinline__ static void candidate(uint32_t k, double h, double disc, double a, double t_min,
+    __device__ __forceinline__ static void candidate(uint32_t k, double h, double disc, const RayDiv& a, double t_min,
                                                      double& closest, uint32_t& best, bool& found, PR& pr) {
         pr.cand_block();
         const double sq = sqrt_g(disc);
-        double ts = (h - sq) / a;
+        double ts = a.div(h - sq);
         bool cand = t_min < ts;
         if (!cand) {
             pr.root2_block();
-            ts = (h + sq) / a;
+            ts = a.div(h + sq);
             cand = t_min < ts;
         }
         if (cand && (ts < closest || (found && ts == closest && k < best))) {
@@ -333,7 +333,8 @@ struct BvhWalker {
         uint32_t best = 0;
         bool found = false;
         const LeafFilter lfilt = LeafFilter::make(a, t_min);
-        for (uint32_t q = 0; q < n_always; ++q) test_always(q, r, a, t_min, lfilt, closest, best, found, pr);
+        const RayDiv ad(a);
+        for (uint32_t q = 0; q < n_always; ++q) test_always(q, r, a, ad, t_min, lfilt, closest, best, found, pr);
         pr.tests(n_always);
 
         // f32 ray for the conservative slab tests (error budget: rt_bvh.cpp)
@@ -433,7 +434,7 @@ struct BvhWalker {
 #if RTZIG_LEAF_FILTER == 0
 #pragma unroll
                 for (int u = 0; u < kLeafBvh; ++u) {
-                    if (disc[u] >= 0) candidate(lf->sid[u], h[u], disc[u], a, t_min, closest, best, found, pr);
+                    if (disc[u] >= 0) candidate(lf->sid[u], h[u], disc[u], ad, t_min, closest, best, found, pr);
                 }
 #else
                 // Compacted candidates: a wave pays a candidate block (sqrt + division) whenever ANY
@@ -467,7 +468,7 @@ struct BvhWalker {
                         any = any || v[u];
                     }
                     if (!any) break;
-                    candidate(kb, hb, db, a, t_min, closest, best, found, pr);
+                    candidate(kb, hb, db, ad, t_min, closest, best, found, pr);
                     if (rd + 1 < kLeafBvh) {
 #pragma unroll
                         for (int u = 0; u < kLeafBvh; ++u) {
