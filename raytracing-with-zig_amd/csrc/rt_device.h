@@ -248,25 +248,6 @@ __device__ __forceinline__ uint64_t sample_key(uint64_t seed_mix, uint64_t pixel
     return sm_mix_hd(seed_mix ^ ((pixel << 32) | (uint64_t)sample));
 }
 
-// One trip of Vec.randomUnitVec's rejection loop (vec.zig:73-79): draws a candidate in the cube and
-// returns whether it is accepted.  The caller finishes with p / sqrt(|p|^2) (true division).
-__device__ __forceinline__ bool ruv_candidate(Rng& g, double& x, double& y, double& z, double& ls) {
-    x = g.range_pm1();
-    y = g.range_pm1();
-    z = g.range_pm1();
-    ls = (x * x + y * y) + z * z;
-    return 1e-160 < ls && ls <= 1;
-}
-
-// Vec.randomInUnitDisk (vec.zig:82-92)
-__device__ __forceinline__ v3 random_in_unit_disk(Rng& g) {
-    for (;;) {
-        const double x = g.range_pm1();
-        const double y = g.range_pm1();
-        if ((x * x + y * y) + 0.0 * 0.0 < 1) return v3{x, y, 0.0};
-    }
-}
-
 // std.math.pow(f64, x, 5) for x in [0, 2] (frexp + repeated squaring == x*((x*x)*(x*x)))
 __device__ __forceinline__ double zig_pow5(double x) {
     if (x == 1.0) return 1.0;

@@ -53,14 +53,18 @@ static_assert(offsetof(KernelParams, center) == 24 && offsetof(KernelParams, pix
                   offsetof(KernelParams, du) == 72 && offsetof(KernelParams, dv) == 96 &&
                   offsetof(KernelParams, ddu) == 120 && offsetof(KernelParams, ddv) == 144 &&
                   offsetof(KernelParams, defocus_angle) == 168,
-              "camera constants: kernarg offsets used by get_ray");
+              "camera constants: kernarg offsets used by camera_start / camera_finish");
 __device__ __forceinline__ double dw2d(uint32_t lo, uint32_t hi) {
     return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
 }
 
-// getRay (camera.zig:187-200) + sampleSquare (:203-209) + defocusDiskSample (:212-215).
-// KernelParams must be the kernel's first argument (kernarg offset 0).
-__device__ __forceinline__ Ray get_ray(uint32_t i, uint32_t j, Rng& g) {
+// getRay (camera.zig:187-200) in two parts around the defocus disk's rejection loop.
+// camera_start: sampleSquare (:203-209) and the pixel sample point.  Without defocus the ray is
+// complete; with defocus r.orig holds the camera center and r.dir the pixel sample point until
+// camera_finish adds the disk sample (defocusDiskSample, :212-215) drawn by path_loop's trip loop.
+// Camera constants are read from the kernarg segment by scalar loads at each use (KernelParams
+// must be the kernel's first argument).
+__device__ __forceinline__ bool camera_start(uint32_t i, uint32_t j, Rng& g, Ray& r) {
     u32x16 A, B;  // dwords 6..21 and 22..37 of KernelParams
     u32x8 C;      // dwords 38..45
     const uint64_t kp = (uint64_t)__builtin_amdgcn_kernarg_segment_ptr();
@@ -75,18 +79,37 @@ __device__ __forceinline__ Ray get_ray(uint32_t i, uint32_t j, Rng& g) {
     const v3 p0 = mk(dw2d(A[6], A[7]), dw2d(A[8], A[9]), dw2d(A[10], A[11]));
     const v3 du = mk(dw2d(A[12], A[13]), dw2d(A[14], A[15]), dw2d(B[0], B[1]));
     const v3 dv = mk(dw2d(B[2], B[3]), dw2d(B[4], B[5]), dw2d(B[6], B[7]));
-    const v3 ddu = mk(dw2d(B[8], B[9]), dw2d(B[10], B[11]), dw2d(B[12], B[13]));
-    const v3 ddv = mk(dw2d(B[14], B[15]), dw2d(C[0], C[1]), dw2d(C[2], C[3]));
     const double defocus_angle = dw2d(C[4], C[5]);
     const double ox = g.uniform() - 0.5;
     const double oy = g.uniform() - 0.5;
     const v3 ps = (p0 + muls(du, (double)i + ox)) + muls(dv, (double)j + oy);
-    v3 origin = center;
-    if (!(defocus_angle <= 0)) {
-        const v3 d = random_in_unit_disk(g);
-        origin = (center + muls(ddu, d.x)) + muls(ddv, d.y);
+    r.orig = center;
+    if (defocus_angle <= 0) {
+        r.dir = ps - center;
+        return false;
     }
-    return Ray{origin, ps - origin};
+    r.dir = ps;
+    return true;  // the disk sample is pending
+}
+// rayOrigin = defocusDiskSample() = (center + defocusDiskU * p.x) + defocusDiskV * p.y;
+// rayDirection = pixelSample - rayOrigin
+__device__ __forceinline__ void camera_finish(double px, double py, Ray& r) {
+    u32x16 A, B;
+    u32x8 C;
+    const uint64_t kp = (uint64_t)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile(
+        "s_load_dwordx16 %0, %3, 24\n\t"
+        "s_load_dwordx16 %1, %3, 88\n\t"
+        "s_load_dwordx8 %2, %3, 152\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=s"(A), "=s"(B), "=s"(C)
+        : "s"(kp));
+    const v3 center = mk(dw2d(A[0], A[1]), dw2d(A[2], A[3]), dw2d(A[4], A[5]));
+    const v3 ddu = mk(dw2d(B[8], B[9]), dw2d(B[10], B[11]), dw2d(B[12], B[13]));
+    const v3 ddv = mk(dw2d(B[14], B[15]), dw2d(C[0], C[1]), dw2d(C[2], C[3]));
+    const v3 origin = (center + muls(ddu, px)) + muls(ddv, py);
+    r.dir = r.dir - origin;
+    r.orig = origin;
 }
 
 // HittableList.hit over Sphere.hit with the exact arithmetic of sphere.zig:27-41.
@@ -520,6 +543,7 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
     uint32_t bounce = 0;
     // pending Lambertian/Metal scatter (waiting for its randomUnitVec), see below
     bool pending = false, sc_metal = false;
+    bool dpend = false;  // camera ray waiting for its defocus-disk sample (camera_start)
     double sc_fuzz = 0;
     v3 sc_nrm = mk(0, 0, 0), sc_refl = mk(0, 0, 0);
     uint64_t rays = 0, nsamples = 0;
@@ -567,7 +591,7 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
                     const uint32_t j = p.row0 + row_local * p.row_step;
                     const uint64_t pixel = (uint64_t)j * W + i;
                     g.seed(sample_key(p.seed_mix, pixel, p.s_begin + s_local));
-                    r = get_ray(i, j, g);
+                    dpend = camera_start(i, j, g, r);
                     att = mk(1, 1, 1);
                     bounce = 0;
                 }
@@ -582,16 +606,67 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
             cyc_refill += t_walk0 - t_top;
         }
 
-        // ---- trace one ray segment per active lane (rayColor's loop body, camera.zig:153-177) --
-        // Lambertian and Metal scatters each draw exactly one Vec.randomUnitVec and nothing else.
-        // Its rejection loop runs for a geometric number of trips per lane (mean 1.91), but a wave
-        // pays the maximum over its lanes (~6).  So the loop is capped at kRuvTrips trips per
-        // iteration: a lane whose candidates were all rejected stays `pending`, skips the next
-        // walk and continues drawing where it stopped.  Every lane still consumes its own stream
-        // in the reference's order, so the bits do not change.
+        // ---- rejection loops, at most kRuvTrips trips per iteration ------------------------------
+        // Two rejection samplers draw from a lane's stream: Vec.randomUnitVec (vec.zig:71-80) for a
+        // pending Lambertian / Metal scatter (3 draws a trip, mean 1.91 trips) and randomInUnitDisk
+        // (vec.zig:82-92) for a new camera ray's defocus sample (2 draws a trip, mean 1.27 trips).
+        // A wave pays the maximum trip count over its lanes, so both share ONE capped loop: a lane
+        // still rejected after kRuvTrips trips stays pending, skips the next walk and continues
+        // drawing where it stopped.  Every lane consumes its own stream in the reference's order,
+        // so the bits do not change.
         bool done = false;
         v3 col = mk(0, 0, 0);
-        if (active && !pending) {
+        double ux = 0, uy = 0, uz = 0, uls = 1;
+        bool got = false, dgot = false;
+        for (int trip = 0; trip < kRuvTrips; ++trip) {
+            const bool wr = pending && !got, wd = dpend && !dgot;
+            if (__ballot(wr || wd) == 0) break;
+            if (wr || wd) {
+                ux = g.range_pm1();
+                uy = g.range_pm1();
+                const double xy = ux * ux + uy * uy;
+                if (wr) {
+                    uz = g.range_pm1();
+                    uls = xy + uz * uz;
+                    got = 1e-160 < uls && uls <= 1;
+                } else {
+                    dgot = xy + 0.0 * 0.0 < 1;  // Vec.lenSquared of (x, y, 0)
+                }
+            }
+        }
+        if (dgot) {
+            camera_finish(ux, uy, r);
+            dpend = false;
+        }
+        if (got) {  // finish the scatter
+            const double l = sqrt_normal(uls);  // |p|^2 in (1e-160, 1] (vec.zig:76)
+            const SharedRcp rl(l);
+            const v3 ruv = mk(rl.div(ux), rl.div(uy), rl.div(uz));  // p / sqrt(|p|^2), true divisions
+            v3 dir;
+            bool absorbed = false;
+            if (!sc_metal) {
+                dir = sc_nrm + ruv;
+                if (near_zero(dir)) dir = sc_nrm;
+            } else {
+                dir = sc_refl + muls(ruv, sc_fuzz);  // unit(reflect(ray.dir, n)) + fuzz * ruv
+                absorbed = !(dot(dir, sc_nrm) > 0);  // absorbed -> black
+            }
+            pending = false;
+            if (absorbed) {
+                done = true;
+            } else {
+                r.dir = dir;
+                ++bounce;
+            }
+        }
+        // ---- trace one ray segment per ready lane (rayColor's loop body, camera.zig:153-177) ---
+        // Lambertian and Metal scatters draw their randomUnitVec in the next iteration's trip loop
+        if constexpr (kProf) {  // the trip loop counts as shading
+            const uint64_t t = __builtin_amdgcn_s_memtime();
+            cyc_shade += t - t_walk0;
+            t_walk0 = t;
+        }
+        if (active && !done && !pending && !dpend) {
             if (bounce >= p.bounce_max) {
                 done = true;  // too many bounces -> black (camera.zig:181)
             } else {
@@ -650,35 +725,6 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
                     r.dir = dir;
                     ++bounce;
                 }
-            }
-        }
-        // Vec.randomUnitVec (vec.zig:71-80): at most kRuvTrips rejection trips this iteration
-        double ux = 0, uy = 0, uz = 0, uls = 1;
-        bool got = false;
-        for (int trip = 0; trip < kRuvTrips; ++trip) {
-            const bool want = pending && !got;
-            if (__ballot(want) == 0) break;
-            if (want) got = ruv_candidate(g, ux, uy, uz, uls);
-        }
-        if (got) {  // finish the scatter
-            const double l = sqrt_normal(uls);  // |p|^2 in (1e-160, 1] (vec.zig:76)
-            const SharedRcp rl(l);
-            const v3 ruv = mk(rl.div(ux), rl.div(uy), rl.div(uz));  // p / sqrt(|p|^2), true divisions
-            v3 dir;
-            bool absorbed = false;
-            if (!sc_metal) {
-                dir = sc_nrm + ruv;
-                if (near_zero(dir)) dir = sc_nrm;
-            } else {
-                dir = sc_refl + muls(ruv, sc_fuzz);  // unit(reflect(ray.dir, n)) + fuzz * ruv
-                absorbed = !(dot(dir, sc_nrm) > 0);  // absorbed -> black
-            }
-            pending = false;
-            if (absorbed) {
-                done = true;
-            } else {
-                r.dir = dir;
-                ++bounce;
             }
         }
         if (done) {
