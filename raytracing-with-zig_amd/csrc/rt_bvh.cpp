@@ -2,10 +2,11 @@
 //
 // Padding rules (all f32 box bounds are rounded OUTWARD from the padded f64 bounds):
 //   pad_k = 2^-17 * (|c_k|_inf + r_k) + 2^-21 * origin_bound + 2^-60
-// The kernel's slab test computes t = fma(bound, inv32, -(o32 * inv32)) in f32.  Its position-space
-// error on each axis is below 2^-24 * (3|bound| + 4|o|) (o -> f32, d -> f32, 1/d, o*inv and the
-// fma, one rounding each).  The |bound| part is covered by 2^-17 (|c| + r) and the |o| part by
-// 2^-21 * origin_bound (= 8 * 2^-24 * bound >= 4 * 2^-24 |o|, a 2x margin).  A sphere's f64 root t_k is a point within ~1e-13 *
+// The kernel's slab test computes t = fma(bound, inv32, -(o32 * inv32)) in f32, inv32 = v_rcp_f32
+// of the f32 direction (1 ulp = 2^-23 relative).  Its position-space error on each axis is below
+// 2^-24 * (4|bound| + 5|o|) (o -> f32, d -> f32, o*inv and the fma: one rounding of 2^-24 each;
+// the reciprocal: 2^-23).  The |bound| part is covered by 2^-17 (|c| + r) and the |o| part by
+// 2^-21 * origin_bound (= 8 * 2^-24 * bound >= 5 * 2^-24 |o|, a 1.6x margin).  A sphere's f64 root t_k is a point within ~1e-13 *
 // (|c|+r) of the true surface, hence inside the padded box, so its leaf is never culled while
 // t_k <= closest; the kernel also widens its `closest` bound by 2^-20 before comparing.
 #include "rt_bvh.hpp"
