@@ -130,6 +130,7 @@ __device__ __forceinline__ uint64_t rotl64(uint64_t x, int k) { return (x << k) 
 // rotl64 by a constant K as two v_alignbit_b32 (the compiler's form is a 64-bit shift, a 32-bit
 // shift and an or): for K < 32 the high word is alignbit(hi, lo, 32 - K), the low word
 // alignbit(lo, hi, 32 - K); K >= 32 swaps the words first.
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 template <int K>
 __device__ __forceinline__ uint64_t rotl64c(uint64_t x) {
     static_assert(K > 0 && K < 64 && K != 32, "rotate");
@@ -142,7 +143,8 @@ __device__ __forceinline__ uint64_t rotl64c(uint64_t x) {
     constexpr uint32_t s = 32u - (uint32_t)(K & 31);
     const uint32_t nhi = __builtin_amdgcn_alignbit(hi, lo, s);
     const uint32_t nlo = __builtin_amdgcn_alignbit(lo, hi, s);
-    return ((uint64_t)nhi << 32) | nlo;
+    // a register pair, not (hi << 32) | lo: the compiler turns that `or` into 64-bit adds
+    return __builtin_bit_cast(uint64_t, u32x2{nlo, nhi});
 }
 
 // a ^ b ^ c of 64-bit words as two gfx950 v_bitop3_b32 (truth table 0x96 = 3-input parity); the
@@ -155,7 +157,7 @@ __device__ __forceinline__ uint32_t xor3_32(uint32_t a, uint32_t b, uint32_t c) 
 __device__ __forceinline__ uint64_t xor3_64(uint64_t a, uint64_t b, uint64_t c) {
     const uint32_t lo = xor3_32((uint32_t)a, (uint32_t)b, (uint32_t)c);
     const uint32_t hi = xor3_32((uint32_t)(a >> 32), (uint32_t)(b >> 32), (uint32_t)(c >> 32));
-    return ((uint64_t)hi << 32) | lo;
+    return __builtin_bit_cast(uint64_t, u32x2{lo, hi});
 }
 
 // SplitMix64.next (zig std/Random/SplitMix64.zig)
@@ -218,7 +220,7 @@ struct Rng {
         const uint32_t t = (hi & 0xfffffu) | (1022u << 20);
         uint32_t ohi;
         asm("v_mad_i32_i24 %0, %1, %2, %3" : "=v"(ohi) : "v"((uint32_t)__builtin_clz(hi)), "s"(-(1 << 20)), "v"(t));
-        return __builtin_bit_cast(double, ((uint64_t)ohi << 32) | (uint32_t)rnd);
+        return __builtin_bit_cast(double, u32x2{(uint32_t)rnd, ohi});
     }
     __device__ __forceinline__ double uniform_slow(uint64_t rnd) {  // p = 2^-12 per draw
         uint64_t lz = rnd ? (uint64_t)__builtin_clzll(rnd) : 64;
