@@ -65,13 +65,14 @@ __device__ __forceinline__ double dw2d(uint32_t lo, uint32_t hi) {
 // Camera constants are read from the kernarg segment by scalar loads at each use (KernelParams
 // must be the kernel's first argument).
 __device__ __forceinline__ bool camera_start(uint32_t i, uint32_t j, Rng& g, Ray& r) {
-    u32x16 A, B;  // dwords 6..21 and 22..37 of KernelParams
-    u32x8 C;      // dwords 38..45
+    u32x16 A;  // dwords 6..21 of KernelParams: center, pixel0, du.x, du.y
+    u32x8 B;   // dwords 22..29: du.z, dv
+    u32x2 C;   // dwords 42..43: defocus_angle
     const uint64_t kp = (uint64_t)__builtin_amdgcn_kernarg_segment_ptr();
     asm volatile(
         "s_load_dwordx16 %0, %3, 24\n\t"
-        "s_load_dwordx16 %1, %3, 88\n\t"
-        "s_load_dwordx8 %2, %3, 152\n\t"
+        "s_load_dwordx8 %1, %3, 88\n\t"
+        "s_load_dwordx2 %2, %3, 168\n\t"
         "s_waitcnt lgkmcnt(0)"
         : "=s"(A), "=s"(B), "=s"(C)
         : "s"(kp));
@@ -79,7 +80,7 @@ __device__ __forceinline__ bool camera_start(uint32_t i, uint32_t j, Rng& g, Ray
     const v3 p0 = mk(dw2d(A[6], A[7]), dw2d(A[8], A[9]), dw2d(A[10], A[11]));
     const v3 du = mk(dw2d(A[12], A[13]), dw2d(A[14], A[15]), dw2d(B[0], B[1]));
     const v3 dv = mk(dw2d(B[2], B[3]), dw2d(B[4], B[5]), dw2d(B[6], B[7]));
-    const double defocus_angle = dw2d(C[4], C[5]);
+    const double defocus_angle = dw2d(C[0], C[1]);
     const double ox = g.uniform() - 0.5;
     const double oy = g.uniform() - 0.5;
     const v3 ps = (p0 + muls(du, (double)i + ox)) + muls(dv, (double)j + oy);
@@ -94,19 +95,18 @@ __device__ __forceinline__ bool camera_start(uint32_t i, uint32_t j, Rng& g, Ray
 // rayOrigin = defocusDiskSample() = (center + defocusDiskU * p.x) + defocusDiskV * p.y;
 // rayDirection = pixelSample - rayOrigin
 __device__ __forceinline__ void camera_finish(double px, double py, Ray& r) {
-    u32x16 A, B;
-    u32x8 C;
+    u32x8 A;   // dwords 6..13: center (+2 unused)
+    u32x16 B;  // dwords 30..45: defocusDiskU, defocusDiskV (+4 unused)
     const uint64_t kp = (uint64_t)__builtin_amdgcn_kernarg_segment_ptr();
     asm volatile(
-        "s_load_dwordx16 %0, %3, 24\n\t"
-        "s_load_dwordx16 %1, %3, 88\n\t"
-        "s_load_dwordx8 %2, %3, 152\n\t"
+        "s_load_dwordx8 %0, %2, 24\n\t"
+        "s_load_dwordx16 %1, %2, 120\n\t"
         "s_waitcnt lgkmcnt(0)"
-        : "=s"(A), "=s"(B), "=s"(C)
+        : "=s"(A), "=s"(B)
         : "s"(kp));
     const v3 center = mk(dw2d(A[0], A[1]), dw2d(A[2], A[3]), dw2d(A[4], A[5]));
-    const v3 ddu = mk(dw2d(B[8], B[9]), dw2d(B[10], B[11]), dw2d(B[12], B[13]));
-    const v3 ddv = mk(dw2d(B[14], B[15]), dw2d(C[0], C[1]), dw2d(C[2], C[3]));
+    const v3 ddu = mk(dw2d(B[0], B[1]), dw2d(B[2], B[3]), dw2d(B[4], B[5]));
+    const v3 ddv = mk(dw2d(B[6], B[7]), dw2d(B[8], B[9]), dw2d(B[10], B[11]));
     const v3 origin = (center + muls(ddu, px)) + muls(ddv, py);
     r.dir = r.dir - origin;
     r.orig = origin;
