@@ -90,6 +90,7 @@ def main():
     ap.add_argument("--output", choices=["linear", "rgb8"], default="linear")
     ap.add_argument("--cpu-spp", type=int, default=4, help="spp of the bounded CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-fast", action="store_true", help="skip the f32 fast-mode side measurement")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL over xGMI, the product) or gloo (rehearsal: several ranks on one GPU)")
     args = ap.parse_args()
@@ -174,6 +175,26 @@ def main():
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed_max = float(t.item())
+    # side measurement (1 GPU only): RT_PRECISION_F32 fast mode on the same frame.  Statistical
+    # parity only (tests/test_fast_mode.py), so it is reported beside `value`, never as it.
+    kname = renderer.kernel_name()  # the timed (parity) kernel, before the fast-mode frames
+    fast = None
+    if world == 1 and not args.no_fast and n_rows:
+        renderer.set_precision("f32")
+        frame()
+        torch.cuda.synchronize()
+        tf0 = time.perf_counter()
+        fk = []
+        for _ in range(2):
+            frame()
+            fk.append(renderer.kernel_times()[0])
+        torch.cuda.synchronize()
+        tf = (time.perf_counter() - tf0) / 2
+        fast = {"value": round(W * H * spp / tf / 1e6, 3), "unit": "Msamples/s", "dtype": "f32",
+                "kernel": renderer.kernel_name(), "kernel_ms_avg": round(float(np.mean(fk)), 3),
+                "note": "RT_PRECISION_F32 fast mode (huge spheres in f64), statistical parity only; "
+                        "not the headline value"}
+        renderer.set_precision("f64")
     st = stats.cpu().tolist()
     rays_per_launch = st[0] / max(1, args.steps)
     samples_per_launch = st[1] / max(1, args.steps)
@@ -223,7 +244,7 @@ def main():
                 # and the matrix pipe alike, so the compute ceiling is the same number
                 "bound": "mfma",
                 "pipe": "f64 VALU (no GEMM-shaped work on this path)",
-                "kernel": renderer.kernel_name(),
+                "kernel": kname,
                 "achieved": round(alg_tf, 3),
                 "peak": FP64_VALU_PEAK_TFLOPS,
                 "unit": "TFLOP/s",
@@ -253,6 +274,7 @@ def main():
             "rays_per_sample": round(rays_per_launch / max(1, samples_per_launch), 4),
             "fixed_costs_ms": {"context_and_scene_upload": round(init_ms, 2)},
             "cpu_baseline": None,
+            "fast_f32": fast,
         }
         if world == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(W, args.aspect, args.cpu_spp)

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 1
+#define RT_ABI_VERSION 2
 
 /* ---- status codes ---------------------------------------------------------------------------- */
 typedef enum rt_status {
@@ -87,12 +87,21 @@ typedef enum rt_output_format {
     RT_OUT_RGB8 = 1        /* fused Color.toRgb (color.zig:63-80): 3 bytes per pixel */
 } rt_output_format;
 
+/* Arithmetic of the sampling kernel. */
+typedef enum rt_precision {
+    RT_PRECISION_F64 = 0,  /* parity: the reference's f64 arithmetic bit for bit (default) */
+    RT_PRECISION_F32 = 1   /* fast: f32 shading / sampling / intersection (huge spheres in f64);
+                              statistical parity only (DESIGN.md "Fast mode") */
+} rt_precision;
+
 typedef struct rt_options {
     int32_t n_gpus;        /* 0 => all visible devices; rows are interleaved j mod n_gpus */
     int32_t device;        /* first device ordinal used */
     uint32_t pixel_stride; /* LINEAR_F64 only: doubles between pixels; 0 => 3. Zig's
                               @Vector(3,f64) has stride 4 (32 bytes), so the shim passes 4 */
     uint32_t output_format;/* rt_output_format */
+    uint32_t precision;    /* rt_precision (0 = parity) */
+    uint32_t reserved;     /* must be 0 */
     uint64_t* stats_out;   /* optional: [0] = rays traced (world.hit calls), [1] = samples */
 } rt_options;
 
@@ -116,6 +125,9 @@ int rt_context_set_scene(rt_context* ctx, const rt_sphere* spheres, size_t n_sph
 int rt_render_rows_async(rt_context* ctx, const rt_camera* cam, uint32_t output_format,
                          uint32_t row0, uint32_t row_step, uint32_t n_rows,
                          void* d_out, void* d_stats, void* stream);
+/* Arithmetic of the context's later renders: rt_precision (default RT_PRECISION_F64).  F32 needs
+ * the BVH walk (any scene whose BVH builds); otherwise the parity kernel runs. */
+int rt_context_set_precision(rt_context* ctx, int precision);
 /* Name of the kernel variant the context launches (for profiling / logs). */
 const char* rt_kernel_name(rt_context* ctx);
 /* Optional per-kernel timing with HIP events recorded on the launch stream around every sample and

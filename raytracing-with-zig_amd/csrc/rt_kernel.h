@@ -58,6 +58,9 @@ struct KernelParams {
     uint32_t pad2;
     FastDiv div_layer;  // / (n_rows * width): item -> (sample, pixel) in the refill
     FastDiv div_width;  // / width: pixel -> (row, column)
+    // f32 copies of the camera constants for the fast (RT_PRECISION_F32) kernel, read by scalar
+    // loads at use: center, pixel0, du, dv, defocusDiskU, defocusDiskV (3 each), defocus_angle
+    float fcam[20];
 };
 
 // BVH (rt_bvh.hpp).  Node = both child boxes (f32, padded outward) + child refs; on the device a
@@ -125,3 +128,8 @@ extern "C" hipError_t rtk_launch_samples_bvh(const rtk::KernelParams* p, const r
                                              void* queue, void* stats, hipStream_t stream, const char** name);
 extern "C" hipError_t rtk_launch_reduce(const rtk::ReduceParams* p, const double* samples,
                                         double* sums, void* out, hipStream_t stream);
+// Fast mode (rt_kernel_fast.hip): the same persistent path loop and BVH in f32 arithmetic, with
+// the always-list (huge / unboundable) spheres tested in f64.  Statistical parity only.
+extern "C" hipError_t rtk_launch_samples_fast(const rtk::KernelParams* p, const rtk::BvhArgs* b, const rtk::GeoRec* geo,
+                                              const rtk::MatRec* mat, double* samples, void* queue, void* stats,
+                                              hipStream_t stream, const char** name);

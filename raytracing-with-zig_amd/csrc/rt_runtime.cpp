@@ -51,6 +51,7 @@ struct rt_context {
     // optional per-kernel timing: event pairs around every sample / reduce launch of the last call
     bool timing = false;
     bool profile = false;  // instrumented kernels: d_stats must hold 8 uint64
+    int precision = RT_PRECISION_F64;
     std::vector<hipEvent_t> events;  // pool; [4c..4c+3] = sample start/stop, reduce start/stop
     uint32_t timed_chunks = 0;
 };
@@ -239,6 +240,15 @@ rtk::KernelParams make_params(const rt_camera* c, uint32_t fmt, uint32_t row0, u
         p.ddv[k] = c->defocus_disk_v[k];
     }
     p.defocus_angle = c->defocus_angle;
+    for (int k = 0; k < 3; k++) {  // f32 copies for the fast kernel
+        p.fcam[0 + k] = (float)c->center[k];
+        p.fcam[3 + k] = (float)c->pixel0[k];
+        p.fcam[6 + k] = (float)c->du[k];
+        p.fcam[9 + k] = (float)c->dv[k];
+        p.fcam[12 + k] = (float)c->defocus_disk_u[k];
+        p.fcam[15 + k] = (float)c->defocus_disk_v[k];
+    }
+    p.fcam[18] = (float)c->defocus_angle;
     p.t_min = c->t_min;
     p.t_max = c->t_max;
     p.seed_mix = rtk::sm_mix_hd(c->seed);
@@ -414,7 +424,10 @@ int rt_render_rows_async(rt_context* ctx, const rt_camera* cam, uint32_t output_
         p.s_begin = (uint32_t)(c * s_chunk);
         p.s_count = (uint32_t)std::min<uint64_t>(s_chunk, cam->samples_per_pixel - p.s_begin);
         if (ctx->timing) HIP_CHECK(hipEventRecord(ctx->events[4 * c + 0], s));
-        if (bvh)
+        if (bvh && ctx->precision == RT_PRECISION_F32)
+            HIP_CHECK(rtk_launch_samples_fast(&p, &ctx->bvh, ctx->d_geo, ctx->d_mat, ctx->d_samples, ctx->d_queue,
+                                              d_stats, s, &ctx->last_kernel));
+        else if (bvh)
             HIP_CHECK(rtk_launch_samples_bvh(&p, &ctx->bvh, ctx->d_geo, ctx->d_mat, ctx->d_samples, ctx->d_queue,
                                              d_stats, s, &ctx->last_kernel));
         else
@@ -440,6 +453,16 @@ int rt_context_enable_timing(rt_context* ctx, int enable) {
     if (!ctx) { rt_set_last_error("null context"); return RT_ERR_INVALID; }
     ctx->timing = enable != 0;
     ctx->timed_chunks = 0;
+    return RT_OK;
+}
+
+int rt_context_set_precision(rt_context* ctx, int precision) {
+    if (!ctx) { rt_set_last_error("null context"); return RT_ERR_INVALID; }
+    if (precision != RT_PRECISION_F64 && precision != RT_PRECISION_F32) {
+        rt_set_last_error("unknown precision");
+        return RT_ERR_INVALID;
+    }
+    ctx->precision = precision;
     return RT_OK;
 }
 
@@ -478,6 +501,10 @@ int rt_render(const rt_camera* cam, const rt_sphere* spheres, size_t n, const rt
     rt_options o{};
     if (opts) o = *opts;
     if (o.output_format > RT_OUT_RGB8) { rt_set_last_error("bad output_format"); return RT_ERR_INVALID; }
+    if (o.precision > RT_PRECISION_F32 || o.reserved != 0) {
+        rt_set_last_error("bad precision / reserved field");
+        return RT_ERR_INVALID;
+    }
     const uint32_t stride = o.pixel_stride ? o.pixel_stride : 3;
     if (o.output_format == RT_OUT_LINEAR_F64 && stride < 3) {
         rt_set_last_error("pixel_stride must be >= 3");
@@ -517,6 +544,7 @@ int rt_render(const rt_camera* cam, const rt_sphere* spheres, size_t n, const rt
         Dev& d = devs[g];
         rc = rt_context_create(first + g, &d.ctx);
         if (!rc) rc = rt_context_set_scene(d.ctx, spheres, n);
+        if (!rc) rc = rt_context_set_precision(d.ctx, (int)o.precision);
         if (rc) { cleanup(); return rc; }
         d.n_rows = (H - (uint32_t)g + (uint32_t)G - 1) / (uint32_t)G;
         const size_t bytes = (size_t)d.n_rows * W * px_bytes;

@@ -17,6 +17,8 @@ RT_DIELECTRIC = 2
 
 RT_OUT_LINEAR_F64 = 0
 RT_OUT_RGB8 = 1
+RT_PRECISION_F64 = 0
+RT_PRECISION_F32 = 1
 
 D3 = C.c_double * 3
 
@@ -61,6 +63,8 @@ class RtOptions(C.Structure):
         ("device", C.c_int32),
         ("pixel_stride", C.c_uint32),
         ("output_format", C.c_uint32),
+        ("precision", C.c_uint32),
+        ("reserved", C.c_uint32),
         ("stats_out", C.POINTER(C.c_uint64)),
     ]
 
@@ -88,7 +92,7 @@ class RtCameraParams(C.Structure):
 SPHERE_SIZE = 80
 CAMERA_SIZE = 200
 CAMERA_PARAMS_SIZE = 144
-OPTIONS_SIZE = 24
+OPTIONS_SIZE = 32
 
 
 def sphere_array(n):

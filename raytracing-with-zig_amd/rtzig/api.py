@@ -141,15 +141,19 @@ class Camera:
     def height(self):
         return self.cam.image_height
 
-    def render(self, n_gpus=0, device=0, output="linear", stats=None):
+    def render(self, n_gpus=0, device=0, output="linear", stats=None, precision="f64"):
         """Camera.render (camera.zig:123-145) on the GPU(s).  Returns a PPM."""
         return PPM(self.width, self.height,
                    render(self.cam, self.scene.world, n_gpus=n_gpus, device=device,
-                          output=output, stats=stats))
+                          output=output, stats=stats, precision=precision))
 
 
-def render(cam, spheres, n_gpus=0, device=0, output="linear", stats=None):
-    """rt_render: whole image into host memory.  linear -> (H, W, 3) f64; rgb8 -> (H, W, 3) u8."""
+_PRECISION = {"f64": abi.RT_PRECISION_F64, "f32": abi.RT_PRECISION_F32}
+
+
+def render(cam, spheres, n_gpus=0, device=0, output="linear", stats=None, precision="f64"):
+    """rt_render: whole image into host memory.  linear -> (H, W, 3) f64; rgb8 -> (H, W, 3) u8.
+    precision: "f64" (parity, bit-exact) or "f32" (fast mode, statistical parity)."""
     lib = load()
     W, H = cam.image_width, cam.image_height
     if output == "linear":
@@ -162,7 +166,7 @@ def render(cam, spheres, n_gpus=0, device=0, output="linear", stats=None):
         raise ValueError(output)
     st = (C.c_uint64 * 2)()
     opts = RtOptions(n_gpus=n_gpus, device=device, pixel_stride=3, output_format=fmt,
-                     stats_out=C.cast(st, C.POINTER(C.c_uint64)))
+                     precision=_PRECISION[precision], stats_out=C.cast(st, C.POINTER(C.c_uint64)))
     n = len(spheres)
     arr = spheres if isinstance(spheres, C.Array) else (RtSphere * n)(*spheres)
     check("rt_render", lib.rt_render(C.byref(cam), arr, n, C.byref(opts),
@@ -196,6 +200,10 @@ class DeviceRenderer:
               self.lib.rt_render_rows_async(self.ctx, C.byref(cam), fmt, row0, row_step, n_rows,
                                             C.c_void_p(d_out_ptr), C.c_void_p(d_stats_ptr or 0),
                                             C.c_void_p(stream_ptr or 0)))
+
+    def set_precision(self, precision):
+        """"f64" (parity kernel, default) or "f32" (fast mode) for later renders."""
+        check("rt_context_set_precision", self.lib.rt_context_set_precision(self.ctx, _PRECISION[precision]))
 
     def kernel_name(self):
         return self.lib.rt_kernel_name(self.ctx).decode()

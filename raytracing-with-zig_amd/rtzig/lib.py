@@ -22,6 +22,7 @@ EXPORTED = [
     "rt_context_enable_timing",
     "rt_context_kernel_times",
     "rt_context_enable_profile",
+    "rt_context_set_precision",
     "rt_scene_final",
     "rt_scene_chapter13",
     "rt_camera_build",
@@ -61,6 +62,7 @@ def _declare(lib):
         "rt_context_enable_timing": (C.c_int, [vp, C.c_int]),
         "rt_context_kernel_times": (C.c_int, [vp, P(C.c_double), P(C.c_double)]),
         "rt_context_enable_profile": (C.c_int, [vp, C.c_int]),
+        "rt_context_set_precision": (C.c_int, [vp, C.c_int]),
         "rt_scene_final": (C.c_int, [C.c_uint64, P(RtSphere), C.c_size_t, P(C.c_size_t),
                                      P(C.c_uint64)]),
         "rt_scene_chapter13": (C.c_int, [P(RtSphere), C.c_size_t, P(C.c_size_t)]),
