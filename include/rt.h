@@ -139,7 +139,8 @@ int rt_context_kernel_times(rt_context* ctx, double* sample_ms, double* reduce_m
  * uint64: {rays, samples, sphere tests executed, BVH node visits, wave-cycles in queue refill,
  * wave-cycles in the closest-hit walk, wave-cycles in shading, wave-iterations of the BVH inner
  * (internal-node) loop, wave-iterations of BVH leaf rounds, wave-level candidate blocks (sqrt +
- * root division), wave-level second-root divisions, 0...}.  Counts 0-3 are exact and
+ * root division), wave-level second-root divisions, node visits of camera rays, sphere tests of
+ * camera rays, 0...}.  Counts 0-3 are exact and
  * deterministic; the cycles and wave-iteration counts are diagnostics. */
 int rt_context_enable_profile(rt_context* ctx, int enable);
 

@@ -189,6 +189,7 @@ struct Prof {
 template <>
 struct Prof<true> {
     uint64_t n_tests = 0, n_visits = 0;
+    uint64_t cam_visits = 0, cam_tests = 0;  // of camera rays (bounce 0)
     uint64_t w_inner = 0, w_leaf = 0;  // wave-level iterations (counted by the first active lane)
     uint64_t w_cand = 0, w_root2 = 0;  // wave-level candidate blocks (sqrt + root1 division) / root2 divisions
     __device__ __forceinline__ void tests(uint32_t n) { n_tests += n; }
@@ -673,7 +674,12 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
             } else {
                 double t;
                 ++rays;
+                uint64_t v0 = 0, t0 = 0;
+                if constexpr (kProf) { v0 = pr.n_visits; t0 = pr.n_tests; }
                 const int k = walk(r, p.t_min, p.t_max, &t, pr);
+                if constexpr (kProf) {
+                    if (bounce == 0) { pr.cam_visits += pr.n_visits - v0; pr.cam_tests += pr.n_tests - t0; }
+                }
                 if constexpr (kProf) t_walk1 = __builtin_amdgcn_s_memtime();
                 // Three branches below need a unit vector: the sky (unit(ray.dir).y), the
                 // dielectric (unit(ray.dir)) and the metal (unit(reflect(ray.dir, n))).  Each is a
@@ -769,6 +775,15 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
             for (int off = 32; off > 0; off >>= 1) {
                 nt += __shfl_xor(nt, off, 64);
                 nv += __shfl_xor(nv, off, 64);
+            }
+            uint64_t cv = pr.cam_visits, ct = pr.cam_tests;
+            for (int off = 32; off > 0; off >>= 1) {
+                cv += __shfl_xor(cv, off, 64);
+                ct += __shfl_xor(ct, off, 64);
+            }
+            if (lane == 0) {
+                atomicAdd(&stats[11], (unsigned long long)cv);
+                atomicAdd(&stats[12], (unsigned long long)ct);
             }
             uint64_t wi = pr.w_inner, wl = pr.w_leaf, wc = pr.w_cand, w2 = pr.w_root2;
             for (int off = 32; off > 0; off >>= 1) {

@@ -53,6 +53,10 @@ for v in args.variants.split():
         "lane_util_inner": round(s[3] / max(1, s[7] * 64), 4),
         "wave_cand_blocks_per_wave_iter": round(s[9] / max(1, s[0] / 64), 3),
         "wave_root2_blocks_per_wave_iter": round(s[10] / max(1, s[0] / 64), 3),
+        "camera_ray_node_visits": round(s[11] / max(1, s[1]), 3),
+        "camera_ray_sphere_tests": round(s[12] / max(1, s[1]), 3),
+        "secondary_ray_node_visits": round((s[3] - s[11]) / max(1, s[0] - s[1]), 3),
+        "secondary_ray_sphere_tests": round((s[2] - s[12]) / max(1, s[0] - s[1]), 3),
         "cycle_split": {"refill": round(s[4] / cyc, 4), "walk": round(s[5] / cyc, 4), "shade": round(s[6] / cyc, 4)},
         "raw": s,
     }
