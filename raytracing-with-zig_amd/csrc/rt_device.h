@@ -251,6 +251,24 @@ __device__ __forceinline__ uint64_t sample_key(uint64_t seed_mix, uint64_t pixel
     return sm_mix_hd(seed_mix ^ ((pixel << 32) | (uint64_t)sample));
 }
 
+// Work-queue claim size (guided self-scheduling): a wave claims kChunk items while plenty remain
+// and ever smaller chunks (down to one item per lane) as the queue drains, so waves run out of
+// work within a few path lengths of each other.  `seen` = the end of the wave's previous claim
+// (a lower bound on the queue position), `nwaves` = waves in the grid.
+#ifndef RTZIG_GUIDED
+#define RTZIG_GUIDED 1
+#endif
+__device__ __forceinline__ uint64_t guided_chunk(uint64_t total, uint64_t seen, uint64_t nwaves, uint64_t max_chunk) {
+#if RTZIG_GUIDED
+    const uint64_t rem = total > seen ? total - seen : 0;
+    uint64_t c = (rem / (2 * nwaves)) & ~63ull;
+    return c < 64 ? 64 : (c > max_chunk ? max_chunk : c);
+#else
+    (void)total; (void)seen; (void)nwaves;
+    return max_chunk;
+#endif
+}
+
 // std.math.pow(f64, x, 5) for x in [0, 2] (frexp + repeated squaring == x*((x*x)*(x*x)))
 __device__ __forceinline__ double zig_pow5(double x) {
     if (x == 1.0) return 1.0;

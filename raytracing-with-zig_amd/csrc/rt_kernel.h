@@ -10,7 +10,7 @@ namespace rtk {
 
 constexpr int kBlock = 256;                // 4 waves of 64 lanes
 constexpr uint32_t kMaxLdsSpheres = 2048;  // 64 KiB of LDS geometry; above this, read from global
-constexpr uint32_t kChunk = 2048;          // work items a wave claims per queue fetch
+constexpr uint32_t kChunk = 2048;          // work items a wave claims per queue fetch (at most: guided_chunk)
 constexpr uint32_t kPad = 4;               // sphere list padded to a multiple of this (sentinels)
 #ifndef RTZIG_RUV_TRIPS
 #define RTZIG_RUV_TRIPS 3
@@ -133,3 +133,5 @@ extern "C" hipError_t rtk_launch_reduce(const rtk::ReduceParams* p, const double
 extern "C" hipError_t rtk_launch_samples_fast(const rtk::KernelParams* p, const rtk::BvhArgs* b, const rtk::GeoRec* geo,
                                               const rtk::MatRec* mat, double* samples, void* queue, void* stats,
                                               hipStream_t stream, const char** name);
+// Resident blocks of `kernel` on the current device (CUs x occupancy), cached (rt_kernel.hip).
+extern "C" hipError_t rtk_resident_blocks(const void* kernel, int block, size_t shmem, uint32_t* blocks);

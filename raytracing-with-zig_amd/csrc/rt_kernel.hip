@@ -30,6 +30,8 @@
 #include <cstdlib>
 #include <climits>
 #include <cstring>
+#include <mutex>
+#include <vector>
 
 #include "rt_device.h"
 #include "rt_kernel.h"
@@ -531,6 +533,7 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
     const uint32_t P = p.n_rows * W;           // pixels per sample layer
     const uint64_t total = (uint64_t)P * p.s_count;
     const uint32_t lane = lane_id();
+    const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x / 64);
 
     // wave-uniform queue window [cur, end)
     uint64_t cur = 0, end = 0;
@@ -551,6 +554,8 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
     uint64_t rays = 0, nsamples = 0;
     Prof<kProf> pr;
     uint64_t cyc_refill = 0, cyc_walk = 0, cyc_shade = 0;  // wave-uniform (kProf only)
+    uint64_t rt_start = 0, rt_drain = 0;  // s_memrealtime (100 MHz) at start / first empty claim (kProf only)
+    if constexpr (kProf) rt_start = __builtin_amdgcn_s_memrealtime();
 
     while (true) {
         uint64_t t_top = 0;
@@ -559,15 +564,17 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
         uint64_t needy = __ballot(!active);
         while (needy != 0 && !drained) {
             if (cur >= end) {
+                const uint64_t chunk = rtk::guided_chunk(total, end, nwaves, kChunk);
                 unsigned long long base = 0;
-                if (lane == 0) base = atomicAdd(queue, (unsigned long long)kChunk);
+                if (lane == 0) base = atomicAdd(queue, (unsigned long long)chunk);
                 base = __shfl(base, 0, 64);
                 if (base >= total) {
                     drained = true;
+                    if constexpr (kProf) rt_drain = __builtin_amdgcn_s_memrealtime();
                     break;
                 }
                 cur = base;
-                end = base + kChunk < total ? base + kChunk : total;
+                end = base + chunk < total ? base + chunk : total;
             }
             const uint64_t avail = end - cur;
             const uint32_t want = (uint32_t)__popcll(needy);
@@ -784,6 +791,12 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
             if (lane == 0) {
                 atomicAdd(&stats[11], (unsigned long long)cv);
                 atomicAdd(&stats[12], (unsigned long long)ct);
+                // kernel timeline on the constant 100 MHz clock: latest wave start, earliest queue
+                // drain, latest wave end (the host reads [13..15]; 0 = unset, so min via ~x)
+                const uint64_t rt_end = __builtin_amdgcn_s_memrealtime();
+                atomicMax(&stats[13], (unsigned long long)rt_start);
+                atomicMax(&stats[14], (unsigned long long)~rt_drain);
+                atomicMax(&stats[15], (unsigned long long)rt_end);
             }
             uint64_t wi = pr.w_inner, wl = pr.w_leaf, wc = pr.w_cand, w2 = pr.w_root2;
             for (int off = 32; off > 0; off >>= 1) {
@@ -900,18 +913,50 @@ __global__ __launch_bounds__(256) void reduce_kernel(ReduceParams p, const doubl
 // ------------------------------------------------------------------------------------------------
 // launch wrappers (called from rt_runtime.cpp)
 // ------------------------------------------------------------------------------------------------
+// A persistent grid: as many blocks as can be resident (CUs x blocks per CU).  If the occupancy
+// query over-reports, the surplus blocks start late and simply find less work.  The device queries
+// (and the dynamic-LDS attribute above 64 KiB) are cached per (device, kernel, block, LDS bytes):
+// they cost host time between the launch's start event and the kernel, which at 8 GPUs (~9 ms
+// frames) is not negligible.
+extern "C" hipError_t rtk_resident_blocks(const void* kernel, int block, size_t shmem, uint32_t* blocks) {
+    struct Entry {
+        int dev;
+        const void* kernel;
+        int block;
+        size_t shmem;
+        uint32_t blocks;
+    };
+    static std::mutex mu;
+    static std::vector<Entry> cache;
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    std::lock_guard<std::mutex> lock(mu);
+    for (const Entry& c : cache)
+        if (c.dev == dev && c.kernel == kernel && c.block == block && c.shmem == shmem) {
+            *blocks = c.blocks;
+            return hipSuccess;
+        }
+    if (shmem > 64 * 1024) {
+        e = hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shmem);
+        if (e != hipSuccess) return e;
+    }
+    int cus = 0, per_cu = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, block, shmem) != hipSuccess || per_cu <= 0)
+        per_cu = 1;
+    cache.push_back(Entry{dev, kernel, block, shmem, (uint32_t)(cus * per_cu)});
+    *blocks = (uint32_t)(cus * per_cu);
+    return hipSuccess;
+}
+
 namespace {
 
-// A persistent grid: as many blocks as can be resident (CUs x blocks per CU).  If the occupancy
-// query over-reports, the surplus blocks start late and simply find less work.
 template <typename K>
 uint32_t persistent_blocks(K kernel, size_t shmem) {
-    int dev = 0, cus = 0, per_cu = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return 1024;
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, rtk::kBlock, shmem) != hipSuccess || per_cu <= 0)
-        per_cu = 4;
-    return (uint32_t)(cus * per_cu);
+    uint32_t b = 0;
+    if (rtk_resident_blocks((const void*)kernel, rtk::kBlock, shmem, &b) != hipSuccess) return 1024;
+    return b;
 }
 
 template <bool kLds, int U, int kWaves>
@@ -992,16 +1037,10 @@ extern "C" hipError_t rtk_launch_samples_bvh(const rtk::KernelParams* p, const r
     auto* st = (unsigned long long*)stats;
     auto* qu = (unsigned long long*)queue;
     auto launch = [&](auto kernel, const char* nm) -> hipError_t {
-        if (shmem > 64 * 1024) {
-            hipError_t ea = hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shmem);
-            if (ea != hipSuccess) return ea;
-        }
-        int dev = 0, cus = 0, per_cu = 0;
-        if (hipGetDevice(&dev) != hipSuccess) dev = 0;
-        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kBlockBvh, shmem) != hipSuccess || per_cu <= 0)
-            per_cu = 2;
-        const uint64_t cap = (uint64_t)cus * per_cu;
+        uint32_t cap32 = 0;
+        const hipError_t ea = rtk_resident_blocks((const void*)kernel, kBlockBvh, shmem, &cap32);
+        if (ea != hipSuccess) return ea;
+        const uint64_t cap = cap32;
         const uint32_t blocks = (uint32_t)(need < cap ? need : cap);
         if (name) *name = nm;
         hipLaunchKernelGGL(kernel, dim3(blocks), dim3(kBlockBvh), shmem, stream, *p, *b, geo, mat, samples, qu, st);

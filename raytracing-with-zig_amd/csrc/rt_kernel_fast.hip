@@ -284,6 +284,7 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
     const uint32_t P = p.n_rows * W;
     const uint64_t total = (uint64_t)P * p.s_count;
     const uint32_t lane = lane_id();
+    const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x / 64);
     const float t_min = (float)p.t_min, t_max = (float)p.t_max;
 
     uint64_t cur = 0, end = 0;
@@ -302,15 +303,16 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
         uint64_t needy = __ballot(!active);
         while (needy != 0 && !drained) {
             if (cur >= end) {
+                const uint64_t chunk = rtk::guided_chunk(total, end, nwaves, kChunk);
                 unsigned long long base = 0;
-                if (lane == 0) base = atomicAdd(queue, (unsigned long long)kChunk);
+                if (lane == 0) base = atomicAdd(queue, (unsigned long long)chunk);
                 base = __shfl(base, 0, 64);
                 if (base >= total) {
                     drained = true;
                     break;
                 }
                 cur = base;
-                end = base + kChunk < total ? base + kChunk : total;
+                end = base + chunk < total ? base + chunk : total;
             }
             const uint64_t avail = end - cur;
             const uint32_t want = (uint32_t)__popcll(needy);
@@ -503,16 +505,10 @@ extern "C" hipError_t rtk_launch_samples_fast(const rtk::KernelParams* p, const 
     hipError_t e = hipMemsetAsync(queue, 0, sizeof(unsigned long long), stream);
     if (e != hipSuccess) return e;
     auto launch = [&](auto kernel, const char* nm) -> hipError_t {
-        if (shmem > 64 * 1024) {
-            hipError_t ea = hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shmem);
-            if (ea != hipSuccess) return ea;
-        }
-        int dev = 0, cus = 0, per_cu = 0;
-        if (hipGetDevice(&dev) != hipSuccess) dev = 0;
-        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kBlockBvh, shmem) != hipSuccess || per_cu <= 0)
-            per_cu = 2;
-        const uint64_t cap = (uint64_t)cus * per_cu;
+        uint32_t cap32 = 0;
+        const hipError_t ea = rtk_resident_blocks((const void*)kernel, kBlockBvh, shmem, &cap32);
+        if (ea != hipSuccess) return ea;
+        const uint64_t cap = cap32;
         const uint32_t blocks = (uint32_t)(need < cap ? need : cap);
         if (name) *name = nm;
         hipLaunchKernelGGL(kernel, dim3(blocks), dim3(kBlockBvh), shmem, stream, *p, *b, geo, mat, samples,

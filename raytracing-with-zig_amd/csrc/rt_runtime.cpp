@@ -386,7 +386,9 @@ int rt_render_rows_async(rt_context* ctx, const rt_camera* cam, uint32_t output_
     // Chunk the samples so that [s_count][P][3] doubles fit the workspace budget.
     const uint64_t P = (uint64_t)n_rows * cam->image_width;
     const uint64_t layer = P * 3 * sizeof(double);
-    uint64_t s_chunk = workspace_budget() / layer;
+    // (the free-memory query is skipped when the whole frame fits the workspace already allocated)
+    const bool fits = ctx->d_samples && ctx->samples_bytes / layer >= cam->samples_per_pixel;
+    uint64_t s_chunk = fits ? cam->samples_per_pixel : workspace_budget() / layer;
     if (s_chunk < 1) s_chunk = 1;
     if (s_chunk > cam->samples_per_pixel) s_chunk = cam->samples_per_pixel;
     if (s_chunk * P > 0xffffffffULL) s_chunk = 0xffffffffULL / P;  // kernel item index is 32-bit

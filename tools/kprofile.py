@@ -20,6 +20,7 @@ ap.add_argument("--width", type=int, default=1200)
 ap.add_argument("--aspect", type=float, default=1.5)
 ap.add_argument("--spp", type=int, default=100)
 ap.add_argument("--variants", default="bvh smem_u4")
+ap.add_argument("--rows", default=None, help="row0:step:n (rank rehearsal), default: the whole image")
 ap.add_argument("--out", default=None)
 args = ap.parse_args()
 
@@ -28,18 +29,20 @@ H, W = cam.height, cam.width
 r = rtzig.DeviceRenderer(0)
 r.set_scene(cam.scene.world)
 r.enable_timing(True)
-out = torch.empty((H, W, 3), dtype=torch.float64, device="cuda:0")
+row0, step, n_rows = (0, 1, H) if args.rows is None else tuple(int(x) for x in args.rows.split(":"))
+rows = dict(row0=row0, row_step=step, n_rows=n_rows)
+out = torch.empty((n_rows, W, 3), dtype=torch.float64, device="cuda:0")
 stats = torch.zeros(16, dtype=torch.int64, device="cuda:0")
 res = {"config": f"{W}x{H} {args.spp}spp, {len(cam.scene.world)} spheres", "variants": {}}
 for v in args.variants.split():
     os.environ["RTZIG_KERNEL"] = v
     r.enable_profile(False)
-    r.render_rows_async(cam.cam, out.data_ptr())
+    r.render_rows_async(cam.cam, out.data_ptr(), **rows)
     torch.cuda.synchronize()
     plain_ms, _ = r.kernel_times()
     r.enable_profile(True)
     stats.zero_()
-    r.render_rows_async(cam.cam, out.data_ptr(), d_stats_ptr=stats.data_ptr())
+    r.render_rows_async(cam.cam, out.data_ptr(), d_stats_ptr=stats.data_ptr(), **rows)
     torch.cuda.synchronize()
     prof_ms, _ = r.kernel_times()
     s = [int(x) for x in stats.cpu().tolist()]
@@ -57,6 +60,10 @@ for v in args.variants.split():
         "camera_ray_sphere_tests": round(s[12] / max(1, s[1]), 3),
         "secondary_ray_node_visits": round((s[3] - s[11]) / max(1, s[0] - s[1]), 3),
         "secondary_ray_sphere_tests": round((s[2] - s[12]) / max(1, s[0] - s[1]), 3),
+        "timeline_us": {"last_wave_start_to_first_drain": round(((~s[14] & (2**64 - 1)) - s[13]) / 100, 1)
+                        if s[14] else None,
+                        "first_drain_to_last_wave_end": round((s[15] - (~s[14] & (2**64 - 1))) / 100, 1)
+                        if s[14] else None},
         "cycle_split": {"refill": round(s[4] / cyc, 4), "walk": round(s[5] / cyc, 4), "shade": round(s[6] / cyc, 4)},
         "raw": s,
     }
