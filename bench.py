@@ -129,9 +129,7 @@ def main():
     torch.cuda.synchronize()
     init_ms = (time.perf_counter() - t_init) * 1e3
 
-    kernel_ms = []   # per timed frame: (sample_kernel_ms, reduce_kernel_ms) from HIP events
-
-    def frame(stats_ptr=None, timed=False):
+    def frame(stats_ptr=None):
         if n_rows:
             renderer.render_rows_async(cam.cam, out.data_ptr(), row0=row0, row_step=step,
                                        n_rows=n_rows, output=args.output, d_stats_ptr=stats_ptr,
@@ -140,8 +138,6 @@ def main():
             img = rdist.gather_image(out.cpu(), H, rank, world)  # gloo gathers host tensors
         else:
             img = rdist.gather_image(out, H, rank, world)
-        if timed and n_rows:
-            kernel_ms.append(renderer.kernel_times())
         return img
 
     for _ in range(args.warmup):
@@ -157,6 +153,9 @@ def main():
         renderer.enable_profile(False)
     prof = [int(x) for x in pstats.cpu().tolist()]
     stats.zero_()
+    # HIP events around every sample / reduce launch of the timed frames, on the launch stream; read
+    # back once after the timed region, so no frame waits on the host
+    renderer.enable_timing(True)
 
     if world > 1:
         dist.barrier()
@@ -164,7 +163,7 @@ def main():
     t0 = time.perf_counter()
     img = None
     for k in range(args.steps):
-        img = frame(stats.data_ptr(), timed=True)
+        img = frame(stats.data_ptr())
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -178,18 +177,19 @@ def main():
     # side measurement (1 GPU only): RT_PRECISION_F32 fast mode on the same frame.  Statistical
     # parity only (tests/test_fast_mode.py), so it is reported beside `value`, never as it.
     kname = renderer.kernel_name()  # the timed (parity) kernel, before the fast-mode frames
+    k_sum, r_sum, _ = renderer.kernel_times_total() if n_rows else (0.0, 0.0, 0)
     fast = None
     if world == 1 and not args.no_fast and n_rows:
         renderer.set_precision("f32")
         frame()
         torch.cuda.synchronize()
+        renderer.enable_timing(True)
         tf0 = time.perf_counter()
-        fk = []
         for _ in range(2):
             frame()
-            fk.append(renderer.kernel_times()[0])
         torch.cuda.synchronize()
         tf = (time.perf_counter() - tf0) / 2
+        fk = [renderer.kernel_times_total()[0] / 2]
         fast = {"value": round(W * H * spp / tf / 1e6, 3), "unit": "Msamples/s", "dtype": "f32",
                 "kernel": renderer.kernel_name(), "kernel_ms_avg": round(float(np.mean(fk)), 3),
                 "note": "RT_PRECISION_F32 fast mode (huge spheres in f64), statistical parity only; "
@@ -202,8 +202,8 @@ def main():
     if rank == 0:
         total_samples = W * H * spp * args.steps
         value = total_samples / elapsed_max / 1e6
-        k_avg_s = float(np.mean([a for a, _ in kernel_ms])) / 1e3   # sample_kernel only
-        r_avg_ms = float(np.mean([b for _, b in kernel_ms]))
+        k_avg_s = k_sum / args.steps / 1e3   # sample_kernel only, per frame
+        r_avg_ms = r_sum / args.steps
         # roofline.achieved follows the contract: ALGORITHMIC work = SURVEY §8(d)'s per-unit figure
         # (17 FLOP per ray-sphere candidate test) x units (485 spheres x rays).  The BVH walk returns
         # the same bits while executing ~2% of those tests, so frac can exceed 1; the work the kernel

@@ -135,6 +135,10 @@ const char* rt_kernel_name(rt_context* ctx);
  * summed durations (ms) of the most recent rt_render_rows_async call. */
 int rt_context_enable_timing(rt_context* ctx, int enable);
 int rt_context_kernel_times(rt_context* ctx, double* sample_ms, double* reduce_ms);
+/* The same summed over every chunk of every call since timing was (re)enabled (at most 1024 chunks;
+ * beyond that the totals restart), so a caller can time many frames without a host sync per frame.
+ * *n_chunks = the number of sample-kernel launches summed. */
+int rt_context_kernel_times_total(rt_context* ctx, double* sample_ms, double* reduce_ms, uint32_t* n_chunks);
 /* Instrumented kernels (diagnostics): when enabled, `d_stats` of rt_render_rows_async must hold 16
  * uint64: {rays, samples, sphere tests executed, BVH node visits, wave-cycles in queue refill,
  * wave-cycles in the closest-hit walk, wave-cycles in shading, wave-iterations of the BVH inner

@@ -791,10 +791,10 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
             if (lane == 0) {
                 atomicAdd(&stats[11], (unsigned long long)cv);
                 atomicAdd(&stats[12], (unsigned long long)ct);
-                // kernel timeline on the constant 100 MHz clock: latest wave start, earliest queue
-                // drain, latest wave end (the host reads [13..15]; 0 = unset, so min via ~x)
+                // kernel timeline on the constant 100 MHz clock: earliest wave start, earliest queue
+                // drain, latest wave end (the host reads [13..15]; 0 = unset, so min via max of ~x)
                 const uint64_t rt_end = __builtin_amdgcn_s_memrealtime();
-                atomicMax(&stats[13], (unsigned long long)rt_start);
+                atomicMax(&stats[13], (unsigned long long)~rt_start);
                 atomicMax(&stats[14], (unsigned long long)~rt_drain);
                 atomicMax(&stats[15], (unsigned long long)rt_end);
             }

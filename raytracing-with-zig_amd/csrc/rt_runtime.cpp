@@ -52,11 +52,18 @@ struct rt_context {
     bool timing = false;
     bool profile = false;  // instrumented kernels: d_stats must hold 8 uint64
     int precision = RT_PRECISION_F64;
-    std::vector<hipEvent_t> events;  // pool; [4c..4c+3] = sample start/stop, reduce start/stop
+    // event pool: every timed chunk of every call takes the next 4 events (sample start/stop,
+    // reduce start/stop); `call_first` / `timed_chunks` locate the last call's, `log_used` counts
+    // the chunks recorded since timing was (re)enabled (rt_context_kernel_times_total)
+    std::vector<hipEvent_t> events;
+    uint32_t call_first = 0;
     uint32_t timed_chunks = 0;
+    uint32_t log_used = 0;
 };
 
 namespace {
+
+constexpr uint32_t kMaxTimedChunks = 1024;  // event-pool bound of rt_context_kernel_times_total
 
 int hip_fail(hipError_t e, const char* what) {
     rt_set_last_error(std::string(what) + ": " + hipGetErrorString(e));
@@ -402,7 +409,10 @@ int rt_render_rows_async(rt_context* ctx, const rt_camera* cam, uint32_t output_
     if (rc) return rc;
 
     if (ctx->timing) {
-        while (ctx->events.size() < 4 * (size_t)n_chunks) {
+        if (ctx->log_used + n_chunks > kMaxTimedChunks) ctx->log_used = 0;  // wrap: totals restart
+        ctx->call_first = ctx->log_used;
+        ctx->log_used += n_chunks;
+        while (ctx->events.size() < 4 * (size_t)ctx->log_used) {
             hipEvent_t e;
             HIP_CHECK(hipEventCreate(&e));
             ctx->events.push_back(e);
@@ -425,7 +435,7 @@ int rt_render_rows_async(rt_context* ctx, const rt_camera* cam, uint32_t output_
     for (uint32_t c = 0; c < n_chunks; c++) {
         p.s_begin = (uint32_t)(c * s_chunk);
         p.s_count = (uint32_t)std::min<uint64_t>(s_chunk, cam->samples_per_pixel - p.s_begin);
-        if (ctx->timing) HIP_CHECK(hipEventRecord(ctx->events[4 * c + 0], s));
+        if (ctx->timing) HIP_CHECK(hipEventRecord(ctx->events[4 * (ctx->call_first + c) + 0], s));
         if (bvh && ctx->precision == RT_PRECISION_F32)
             HIP_CHECK(rtk_launch_samples_fast(&p, &ctx->bvh, ctx->d_geo, ctx->d_mat, ctx->d_samples, ctx->d_queue,
                                               d_stats, s, &ctx->last_kernel));
@@ -435,7 +445,7 @@ int rt_render_rows_async(rt_context* ctx, const rt_camera* cam, uint32_t output_
         else
             HIP_CHECK(rtk_launch_samples(&p, ctx->d_geo, ctx->d_mat, ctx->d_samples, ctx->d_queue, d_stats, s,
                                          &ctx->last_kernel));
-        if (ctx->timing) HIP_CHECK(hipEventRecord(ctx->events[4 * c + 1], s));
+        if (ctx->timing) HIP_CHECK(hipEventRecord(ctx->events[4 * (ctx->call_first + c) + 1], s));
         rtk::ReduceParams rp;
         std::memset(&rp, 0, sizeof rp);
         rp.n_pixels = (uint32_t)P;
@@ -444,9 +454,9 @@ int rt_render_rows_async(rt_context* ctx, const rt_camera* cam, uint32_t output_
         rp.last = c + 1 == n_chunks;
         rp.out_format = output_format;
         rp.scale = cam->pixel_samples_scale;
-        if (ctx->timing) HIP_CHECK(hipEventRecord(ctx->events[4 * c + 2], s));
+        if (ctx->timing) HIP_CHECK(hipEventRecord(ctx->events[4 * (ctx->call_first + c) + 2], s));
         HIP_CHECK(rtk_launch_reduce(&rp, ctx->d_samples, ctx->d_sums, d_out, s));
-        if (ctx->timing) HIP_CHECK(hipEventRecord(ctx->events[4 * c + 3], s));
+        if (ctx->timing) HIP_CHECK(hipEventRecord(ctx->events[4 * (ctx->call_first + c) + 3], s));
     }
     return RT_OK;
 }
@@ -455,6 +465,8 @@ int rt_context_enable_timing(rt_context* ctx, int enable) {
     if (!ctx) { rt_set_last_error("null context"); return RT_ERR_INVALID; }
     ctx->timing = enable != 0;
     ctx->timed_chunks = 0;
+    ctx->call_first = 0;
+    ctx->log_used = 0;
     return RT_OK;
 }
 
@@ -479,7 +491,7 @@ int rt_context_kernel_times(rt_context* ctx, double* sample_ms, double* reduce_m
     if (!ctx->timing || ctx->timed_chunks == 0) { rt_set_last_error("timing not enabled or nothing rendered"); return RT_ERR_INVALID; }
     HIP_CHECK(hipSetDevice(ctx->device));
     double sm = 0, rm = 0;
-    for (uint32_t c = 0; c < ctx->timed_chunks; c++) {
+    for (uint32_t c = ctx->call_first; c < ctx->call_first + ctx->timed_chunks; c++) {
         float a = 0, b = 0;
         HIP_CHECK(hipEventSynchronize(ctx->events[4 * c + 3]));
         HIP_CHECK(hipEventElapsedTime(&a, ctx->events[4 * c + 0], ctx->events[4 * c + 1]));
@@ -489,6 +501,25 @@ int rt_context_kernel_times(rt_context* ctx, double* sample_ms, double* reduce_m
     }
     if (sample_ms) *sample_ms = sm;
     if (reduce_ms) *reduce_ms = rm;
+    return RT_OK;
+}
+
+int rt_context_kernel_times_total(rt_context* ctx, double* sample_ms, double* reduce_ms, uint32_t* n_chunks) {
+    if (!ctx) { rt_set_last_error("null context"); return RT_ERR_INVALID; }
+    if (!ctx->timing) { rt_set_last_error("timing not enabled"); return RT_ERR_INVALID; }
+    HIP_CHECK(hipSetDevice(ctx->device));
+    double sm = 0, rm = 0;
+    for (uint32_t c = 0; c < ctx->log_used; c++) {
+        float a = 0, b = 0;
+        HIP_CHECK(hipEventSynchronize(ctx->events[4 * c + 3]));
+        HIP_CHECK(hipEventElapsedTime(&a, ctx->events[4 * c + 0], ctx->events[4 * c + 1]));
+        HIP_CHECK(hipEventElapsedTime(&b, ctx->events[4 * c + 2], ctx->events[4 * c + 3]));
+        sm += a;
+        rm += b;
+    }
+    if (sample_ms) *sample_ms = sm;
+    if (reduce_ms) *reduce_ms = rm;
+    if (n_chunks) *n_chunks = ctx->log_used;
     return RT_OK;
 }
 

@@ -221,6 +221,13 @@ class DeviceRenderer:
         check("rt_context_kernel_times", self.lib.rt_context_kernel_times(self.ctx, C.byref(a), C.byref(b)))
         return a.value, b.value
 
+    def kernel_times_total(self):
+        """(sample_kernel_ms, reduce_kernel_ms, launches) summed since timing was enabled."""
+        a, b, n = C.c_double(), C.c_double(), C.c_uint32()
+        check("rt_context_kernel_times_total",
+              self.lib.rt_context_kernel_times_total(self.ctx, C.byref(a), C.byref(b), C.byref(n)))
+        return a.value, b.value, n.value
+
     def close(self):
         if self.ctx:
             self.lib.rt_context_destroy(self.ctx)

@@ -21,6 +21,7 @@ EXPORTED = [
     "rt_kernel_name",
     "rt_context_enable_timing",
     "rt_context_kernel_times",
+    "rt_context_kernel_times_total",
     "rt_context_enable_profile",
     "rt_context_set_precision",
     "rt_scene_final",
@@ -61,6 +62,7 @@ def _declare(lib):
         "rt_kernel_name": (C.c_char_p, [vp]),
         "rt_context_enable_timing": (C.c_int, [vp, C.c_int]),
         "rt_context_kernel_times": (C.c_int, [vp, P(C.c_double), P(C.c_double)]),
+        "rt_context_kernel_times_total": (C.c_int, [vp, P(C.c_double), P(C.c_double), P(C.c_uint32)]),
         "rt_context_enable_profile": (C.c_int, [vp, C.c_int]),
         "rt_context_set_precision": (C.c_int, [vp, C.c_int]),
         "rt_scene_final": (C.c_int, [C.c_uint64, P(RtSphere), C.c_size_t, P(C.c_size_t),
