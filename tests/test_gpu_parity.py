@@ -286,3 +286,45 @@ def test_config5_crop_bit_exact(oracle):
         ref, _ = oracle.render_b(cam.cam, cam.scene.world, row0=j, row_step=1, n_rows=1, threads=8)
         assert np.array_equal(buf.cpu().numpy(), ref), j
     r.close()
+
+
+def _soup(seed, scale):
+    rng = np.random.default_rng(seed)
+    n = int(rng.integers(20, 120))
+    arr = (RtSphere * (n + 1))()
+    for k in range(n):
+        arr[k] = RtSphere(center=D3(*(rng.normal(0, 3, 3) * scale)),
+                          radius=float(rng.choice([rng.uniform(0.01, 0.5), rng.uniform(0.5, 3)]) * scale),
+                          material=int(rng.integers(0, 3)), albedo=D3(*rng.uniform(0, 1, 3)),
+                          fuzz=float(rng.uniform(0, 1.2)), refraction_index=float(rng.uniform(0.5, 2.5)))
+    arr[n] = RtSphere(center=D3(0, -1000.5 * scale, 0), radius=1000.0 * scale, material=0, albedo=D3(0.5, 0.5, 0.5))
+    scene = rtzig.Scene.init(seed)
+    scene.world = arr
+    look_from = tuple(rng.normal(0, 8, 3) * scale)
+    cam = (rtzig.Camera.builder(64, 1.5).setScene(scene).setDefocusAngle(float(rng.uniform(0, 3)))
+           .setFocusDist(float(rng.uniform(1, 10)) * scale).setViewport(look_from, (0, 0, 0), float(rng.uniform(20, 90)))
+           .setSamplesPerPixel(3).build())
+    return arr, cam
+
+
+@pytest.mark.parametrize("scale", [1e-70, 1e-40, 1e40, 1e70])
+def test_extreme_scales_bit_exact(oracle, scale):
+    """The exact fast paths of the kernel (unscaled sqrt, shared-reciprocal divisions, the leaf
+    filter, f32 BVH boxes) are guarded by range checks; at these scales the discriminants, |dir|^2
+    and the coordinates leave the guarded ranges (and f32's range), so the lanes take the full
+    correctly rounded sequences and the always-list.  Bits must still equal oracle B."""
+    arr, cam = _soup(11, scale)
+    out, st = gpu_render(cam, arr, n_gpus=1)
+    ref, rays = oracle.render_b(cam.cam, arr, threads=8)
+    assert np.array_equal(out, ref) and st["rays"] == rays
+
+
+@pytest.mark.parametrize("t_min", [0.0, -0.5, 1e-9, 0.25])
+def test_interval_min_variants_bit_exact(oracle, t_min):
+    """Scene.interval.min other than 1e-3 (zero, negative, tiny, large): the leaf filter's margins
+    and the root selection (sphere.zig:35-41) must follow the reference for any t_min."""
+    arr, cam = _soup(12, 1.0)
+    cam.cam.t_min = t_min
+    out, st = gpu_render(cam, arr, n_gpus=1)
+    ref, rays = oracle.render_b(cam.cam, arr, threads=8)
+    assert np.array_equal(out, ref) and st["rays"] == rays
