@@ -253,8 +253,9 @@ __device__ __forceinline__ uint64_t sample_key(uint64_t seed_mix, uint64_t pixel
 
 // Work-queue claim size (guided self-scheduling): a wave claims kChunk items while plenty remain
 // and ever smaller chunks (down to one item per lane) as the queue drains, so waves run out of
-// work within a few path lengths of each other.  `seen` = the end of the wave's previous claim
-// (a lower bound on the queue position), `nwaves` = waves in the grid.
+// work within a few path lengths of each other.  `seen` = an estimate of the queue position,
+// `nwaves` = waves in the grid.  The minimum (256 items, 4 per lane) keeps claims rare: a claim
+// stalls its whole wave for an atomic round trip, and claims of 64 items measured 4% slower.
 #ifndef RTZIG_GUIDED
 #define RTZIG_GUIDED 1
 #endif
@@ -262,7 +263,7 @@ __device__ __forceinline__ uint64_t guided_chunk(uint64_t total, uint64_t seen, 
 #if RTZIG_GUIDED
     const uint64_t rem = total > seen ? total - seen : 0;
     uint64_t c = (rem / (2 * nwaves)) & ~63ull;
-    return c < 64 ? 64 : (c > max_chunk ? max_chunk : c);
+    return c < 256 ? 256 : (c > max_chunk ? max_chunk : c);
 #else
     (void)total; (void)seen; (void)nwaves;
     return max_chunk;

@@ -536,7 +536,7 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
     const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x / 64);
 
     // wave-uniform queue window [cur, end)
-    uint64_t cur = 0, end = 0;
+    uint64_t cur = 0, end = 0, last_chunk = 0;
     bool drained = false;
 
     // per-lane path state
@@ -564,7 +564,10 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
         uint64_t needy = __ballot(!active);
         while (needy != 0 && !drained) {
             if (cur >= end) {
-                const uint64_t chunk = rtk::guided_chunk(total, end, nwaves, kChunk);
+                // guided claim, sized from an estimate of the queue position: this wave's previous
+                // claim plus one such claim by every other wave since (rtk::guided_chunk)
+                const uint64_t chunk = rtk::guided_chunk(total, end + nwaves * last_chunk, nwaves, kChunk);
+                last_chunk = chunk;
                 unsigned long long base = 0;
                 if (lane == 0) base = atomicAdd(queue, (unsigned long long)chunk);
                 base = __shfl(base, 0, 64);

@@ -287,7 +287,7 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
     const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x / 64);
     const float t_min = (float)p.t_min, t_max = (float)p.t_max;
 
-    uint64_t cur = 0, end = 0;
+    uint64_t cur = 0, end = 0, last_chunk = 0;
     bool drained = false;
     bool active = false, pending = false, sc_metal = false, dpend = false;
     uint64_t slot = 0;
@@ -303,7 +303,10 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
         uint64_t needy = __ballot(!active);
         while (needy != 0 && !drained) {
             if (cur >= end) {
-                const uint64_t chunk = rtk::guided_chunk(total, end, nwaves, kChunk);
+                // guided claim, sized from an estimate of the queue position: this wave's previous
+                // claim plus one such claim by every other wave since (rtk::guided_chunk)
+                const uint64_t chunk = rtk::guided_chunk(total, end + nwaves * last_chunk, nwaves, kChunk);
+                last_chunk = chunk;
                 unsigned long long base = 0;
                 if (lane == 0) base = atomicAdd(queue, (unsigned long long)chunk);
                 base = __shfl(base, 0, 64);
@@ -323,7 +326,7 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
                     active = true;
                     const uint32_t it32 = (uint32_t)(cur + rk);
                     uint32_t s_local, q;
-                    if (p.order == 0) {
+                    if (p.order == 0) {  // sample-major: a wave takes 64 neighbouring pixels
                         s_local = rtk::fastdiv(it32, p.div_layer);
                         q = it32 - s_local * P;
                     } else {

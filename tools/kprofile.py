@@ -60,7 +60,7 @@ for v in args.variants.split():
         "camera_ray_sphere_tests": round(s[12] / max(1, s[1]), 3),
         "secondary_ray_node_visits": round((s[3] - s[11]) / max(1, s[0] - s[1]), 3),
         "secondary_ray_sphere_tests": round((s[2] - s[12]) / max(1, s[0] - s[1]), 3),
-        "timeline_us": {"last_wave_start_to_first_drain": round(((~s[14] & (2**64 - 1)) - s[13]) / 100, 1)
+        "timeline_us": {"first_wave_start_to_first_drain": round(((~s[14] & (2**64 - 1)) - (~s[13] & (2**64 - 1))) / 100, 1)
                         if s[14] else None,
                         "first_drain_to_last_wave_end": round((s[15] - (~s[14] & (2**64 - 1))) / 100, 1)
                         if s[14] else None},
