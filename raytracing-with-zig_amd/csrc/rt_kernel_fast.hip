@@ -14,7 +14,7 @@
 // angles; every other sphere's quadratic is well conditioned in f32 at t_min = 1e-3.
 //
 // The RNG stream of a (pixel, sample) is the parity kernel's (rt_sample_key + DefaultPrng.init); a
-// uniform is the top 24 bits of one Xoshiro256++ word.
+// uniform is 24 bits of a Xoshiro256++ word, paired draws take both halves of one word.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -58,9 +58,16 @@ __device__ __forceinline__ f3 refract(f3 v, f3 n, float eta) {
 }
 __device__ __forceinline__ bool near_zero(f3 v) { return v.x < 1e-8f && v.y < 1e-8f && v.z < 1e-8f; }  // vec.zig:26-29
 
-// U[0, 1) from the top 24 bits of one Xoshiro256++ word (exact in f32)
+// U[0, 1) from the top 24 bits of one Xoshiro256++ word (exact in f32); uniform2 takes two from one
+// word (the top 24 bits of each 32-bit half), halving the generator work of paired draws
 __device__ __forceinline__ float uniform(Rng& g) { return (float)(uint32_t)(g.next() >> 40) * 0x1p-24f; }
-__device__ __forceinline__ float range_pm1(Rng& g) { return __builtin_fmaf(2.0f, uniform(g), -1.0f); }
+__device__ __forceinline__ void uniform2(Rng& g, float& a, float& b) {
+    const uint64_t w = g.next();
+    a = (float)(uint32_t)(w >> 40) * 0x1p-24f;
+    b = (float)((uint32_t)w >> 8) * 0x1p-24f;
+}
+__device__ __forceinline__ float pm1(float u) { return __builtin_fmaf(2.0f, u, -1.0f); }
+__device__ __forceinline__ float range_pm1(Rng& g) { return pm1(uniform(g)); }
 
 struct Ray {
     f3 orig, dir;
@@ -89,8 +96,10 @@ __device__ __forceinline__ bool camera_start(uint32_t i, uint32_t j, Rng& g, Ray
     const f3 du = mk(f(A[6]), f(A[7]), f(A[8]));
     const f3 dv = mk(f(A[9]), f(A[10]), f(A[11]));
     const float defocus_angle = f(B[2]);
-    const float ox = uniform(g) - 0.5f;
-    const float oy = uniform(g) - 0.5f;
+    float ox, oy;
+    uniform2(g, ox, oy);
+    ox -= 0.5f;
+    oy -= 0.5f;
     const f3 ps = (p0 + muls(du, (float)i + ox)) + muls(dv, (float)j + oy);
     r.orig = center;
     if (defocus_angle <= 0) {
@@ -357,8 +366,9 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
             const bool wr = pending && !got, wd = dpend && !dgot;
             if (__ballot(wr || wd) == 0) break;
             if (wr || wd) {
-                ux = range_pm1(g);
-                uy = range_pm1(g);
+                uniform2(g, ux, uy);
+                ux = pm1(ux);
+                uy = pm1(uy);
                 const float xy = ux * ux + uy * uy;
                 if (wr) {
                     uz = range_pm1(g);
