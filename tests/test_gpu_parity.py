@@ -328,3 +328,25 @@ def test_interval_min_variants_bit_exact(oracle, t_min):
     out, st = gpu_render(cam, arr, n_gpus=1)
     ref, rays = oracle.render_b(cam.cam, arr, threads=8)
     assert np.array_equal(out, ref) and st["rays"] == rays
+
+
+def test_kernel_times_total_accumulates():
+    """rt_context_kernel_times_total sums the HIP-event times of every launch since timing was
+    enabled (bench.py reads it once after its timed region); per-call times stay available."""
+    import torch
+    cam = rtzig.final_scene_camera(width=120, aspect_ratio=1.5, spp=4)
+    r = rtzig.DeviceRenderer(0)
+    r.set_scene(cam.scene.world)
+    out = torch.zeros((cam.height, cam.width, 3), dtype=torch.float64, device="cuda:0")
+    r.enable_timing(True)
+    per = []
+    for _ in range(3):
+        r.render_rows_async(cam.cam, out.data_ptr())
+        per.append(r.kernel_times())
+    s, red, n = r.kernel_times_total()
+    assert n == 3
+    assert abs(s - sum(a for a, _ in per)) < 1e-3 and abs(red - sum(b for _, b in per)) < 1e-3
+    r.enable_timing(True)  # re-enabling restarts the totals
+    r.render_rows_async(cam.cam, out.data_ptr())
+    assert r.kernel_times_total()[2] == 1
+    r.close()
