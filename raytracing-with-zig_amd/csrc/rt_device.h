@@ -259,11 +259,14 @@ __device__ __forceinline__ uint64_t sample_key(uint64_t seed_mix, uint64_t pixel
 #ifndef RTZIG_GUIDED
 #define RTZIG_GUIDED 1
 #endif
+#ifndef RTZIG_MIN_CHUNK
+#define RTZIG_MIN_CHUNK 256
+#endif
 __device__ __forceinline__ uint64_t guided_chunk(uint64_t total, uint64_t seen, uint64_t nwaves, uint64_t max_chunk) {
 #if RTZIG_GUIDED
     const uint64_t rem = total > seen ? total - seen : 0;
     uint64_t c = (rem / (2 * nwaves)) & ~63ull;
-    return c < 256 ? 256 : (c > max_chunk ? max_chunk : c);
+    return c < RTZIG_MIN_CHUNK ? RTZIG_MIN_CHUNK : (c > max_chunk ? max_chunk : c);
 #else
     (void)total; (void)seen; (void)nwaves;
     return max_chunk;
