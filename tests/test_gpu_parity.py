@@ -350,3 +350,17 @@ def test_kernel_times_total_accumulates():
     r.render_rows_async(cam.cam, out.data_ptr())
     assert r.kernel_times_total()[2] == 1
     r.close()
+
+
+@pytest.mark.parametrize("mb", [3, 5])
+def test_sample_chunked_workspace_bit_exact(oracle, monkeypatch, mb):
+    """A workspace budget smaller than one frame of per-sample colors (RTZIG_WORKSPACE_MB) splits
+    the samples into several launches; the reduce kernel carries the running sums across them in
+    sample order (camera.zig:133-136), so the image must not change."""
+    monkeypatch.setenv("RTZIG_WORKSPACE_MB", str(mb))
+    cam = rtzig.chapter9_camera(spp=7)
+    out, st = gpu_render(cam, cam.scene.world, n_gpus=1)
+    ref, rays = oracle.render_b(cam.cam, cam.scene.world, threads=8)
+    assert np.array_equal(out, ref) and st["rays"] == rays and st["samples"] == 400 * 225 * 7
+    rgb, _ = gpu_render(cam, cam.scene.world, n_gpus=1, output="rgb8")
+    assert np.array_equal(rgb, oracle.to_rgb8(ref))
