@@ -198,21 +198,30 @@ Bvh build(const rt_sphere* spheres, size_t n, double origin_bound) {
         p.sphere = (uint32_t)k;
         B.prims.push_back(p);
     }
-    // Huge spheres (a ground plane of radius 1000) go to the always-list: their box spans the
-    // scene, so in the tree they cost a leaf round for most rays and inflate every ancestor box;
-    // tested up front in lockstep they cost one sphere test per ray and hand the traversal a
-    // tight `closest` to cull against.  Criterion: box surface area >= kAlwaysArea x the area of
-    // the box of all boundable spheres, at most kMaxBig of them (largest first).
+    // Huge and big spheres go to the always-list.  A huge sphere (the final scene's radius-1000
+    // ground) spans the scene: in the tree it costs a leaf round for most rays and inflates every
+    // ancestor box.  A big one (its three radius-1 spheres among radius-0.2 ones) inflates the
+    // boxes of every node above the small spheres it overlaps.  Tested up front in lockstep, each
+    // costs one sphere test per ray and hands the traversal a tight `closest` to cull against.
+    // Criterion: box surface area >= kAlwaysArea x the area of the box of all boundable spheres,
+    // or >= kAlwaysRel x the median sphere box area; at most kMaxBig of them, largest first.
+    // (Config 4: node visits per ray 8.86 -> 6.97, kernel -2%.)
     if (B.prims.size() > (size_t)kLeafMax) {
         double lo[3], hi[3];
         B.bounds(0, B.prims.size(), lo, hi);
         const double total = Builder::area(lo, hi);
-        double frac = kAlwaysArea;
-        if (const char* e = std::getenv("RTZIG_BVH_ALWAYS_AREA")) frac = std::atof(e);  // A/B knob
+        double frac = kAlwaysArea, rel = kAlwaysRel;
+        if (const char* e = std::getenv("RTZIG_BVH_ALWAYS_AREA")) frac = std::atof(e);  // A/B knobs
+        if (const char* e = std::getenv("RTZIG_BVH_ALWAYS_REL")) rel = std::atof(e);
+        std::vector<double> areas(B.prims.size());
+        for (size_t i = 0; i < B.prims.size(); i++) areas[i] = Builder::area(B.prims[i].lo, B.prims[i].hi);
+        std::vector<double> sorted = areas;
+        std::nth_element(sorted.begin(), sorted.begin() + (long)(sorted.size() / 2), sorted.end());
+        const double median = sorted[sorted.size() / 2];
         std::vector<std::pair<double, size_t>> big;
         for (size_t i = 0; i < B.prims.size(); i++) {
-            const double a = Builder::area(B.prims[i].lo, B.prims[i].hi);
-            if (frac > 0 && a >= frac * total) big.push_back({-a, i});
+            const double a = areas[i];
+            if ((frac > 0 && a >= frac * total) || (rel > 0 && a >= rel * median)) big.push_back({-a, i});
         }
         std::sort(big.begin(), big.end());
         if (big.size() > (size_t)kMaxBig) big.resize(kMaxBig);

@@ -23,6 +23,7 @@ namespace rtbvh {
 constexpr int kLeafMax = RTZIG_LEAF;   // spheres per leaf (build knob; A/B on config 4: 2 < 4 < 3 ms, 1 and 8 clearly slower)
 constexpr int kMaxDepth = 16; // tree depth bound == per-lane stack size in the kernel
 constexpr double kAlwaysArea = 0.25;  // box-area fraction above which a sphere is tested always
+constexpr double kAlwaysRel = 10.0;   // ... or box area above this multiple of the median sphere's
 constexpr int kMaxBig = 4;           // at most this many such spheres
 constexpr uint32_t kSentinel = 0xffffffffu;  // slot_to_sphere value of a padding slot
 
