@@ -109,10 +109,10 @@ int validate_spheres(const rt_sphere* s, size_t n) {
     return RT_OK;
 }
 
-// Workspace budget for per-sample colors: RTZIG_WORKSPACE_MB, default 16 GiB (MI355X has 288 GB
+// Workspace budget for per-sample colors: RTZIG_WORKSPACE_MB, default 64 GiB (MI355X has 288 GB
 // of HBM; a whole config-4 frame needs 11.5 GB), never more than 60% of the free memory.
 uint64_t workspace_budget() {
-    uint64_t budget = 16ULL << 30;
+    uint64_t budget = 64ULL << 30;
     if (const char* e = std::getenv("RTZIG_WORKSPACE_MB")) budget = std::strtoull(e, nullptr, 10) << 20;
     size_t free_b = 0, total_b = 0;
     if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b > 0) {
