@@ -216,6 +216,7 @@ def main():
         # sample_kernel HBM bytes: one 24-B f64 color per sample written (the reduce kernel reads
         # them back: +24 B/sample, + the framebuffer)
         alg_bytes = n_rows * W * spp * 24
+        red_bytes = n_rows * W * spp * 24 + n_rows * W * (24 if args.output == "linear" else 3)
         workload = f"final-render {W}x{H} {spp}spp depth50 ({n_spheres} spheres)"
         traffic = pmc_traffic(workload)
         assert img is not None and img.shape[0] == H
@@ -270,6 +271,13 @@ def main():
                 "achieved_GBps": round(alg_bytes / k_avg_s / 1e9, 3),
                 "peak_GBps": HBM_PEAK_GBS,
                 "frac": round(alg_bytes / k_avg_s / 1e9 / HBM_PEAK_GBS, 6),
+                # the ordered per-pixel reduction is the HBM-bound kernel of the path: it reads every
+                # per-sample color once and writes the framebuffer
+                "reduce_kernel": {
+                    "algorithmic_bytes_per_launch": red_bytes,
+                    "achieved_GBps": round(red_bytes / (r_avg_ms / 1e3) / 1e9, 1) if r_avg_ms > 0 else None,
+                    "frac": round(red_bytes / (r_avg_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4) if r_avg_ms > 0 else None,
+                },
             },
             "rays_per_sample": round(rays_per_launch / max(1, samples_per_launch), 4),
             "fixed_costs_ms": {"context_and_scene_upload": round(init_ms, 2)},
