@@ -882,6 +882,7 @@ __global__ __launch_bounds__(256) void reduce_kernel(ReduceParams p, const doubl
     }
     const double* src = samples + 3 * (uint64_t)q;
     const uint64_t stride = 3 * (uint64_t)p.n_pixels;
+#pragma unroll 8
     for (uint32_t s = 0; s < p.s_count; ++s) {
         x = x + src[0];
         y = y + src[1];
