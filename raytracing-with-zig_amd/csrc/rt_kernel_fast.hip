@@ -8,8 +8,8 @@
 // single-instruction reciprocal / rsqrt / sqrt and FMA is allowed.  Parity is statistical
 // (tests/test_fast_mode.py, DESIGN.md "Fast mode").
 //
-// Precision guard: spheres on the BVH's always-list (huge or unboundable, e.g. the final scene's
-// r = 1000 ground, rt_bvh.cpp) are tested in f64.  In f32 a point on a radius-1000 sphere is only
+// Precision guard: huge spheres on the BVH's always-list (radius >= 100 or far out, e.g. the final
+// scene's r = 1000 ground, rt_bvh.cpp) are tested in f64; the big ones (its r = 1 spheres) in f32.  In f32 a point on a radius-1000 sphere is only
 // known to ~6e-5 along the normal, so secondary rays leaving it would re-hit it ("acne") at grazing
 // angles; every other sphere's quadratic is well conditioned in f32 at t_min = 1e-3.
 //
@@ -181,6 +181,24 @@ struct Walker {
             double cl = (double)t_max;
             for (uint32_t q = 0; q < n_always; ++q) {
                 const GeoRec s = ageo[q];
+                if (s.r2 < 1e4 && __builtin_fabs(s.cx) + __builtin_fabs(s.cy) + __builtin_fabs(s.cz) < 1e4) {
+                    // a big but not huge sphere (radius < 100): well conditioned in f32
+                    const float fx = (float)s.cx - r.orig.x, fy = (float)s.cy - r.orig.y, fz = (float)s.cz - r.orig.z;
+                    const float fa = len_sq(r.dir);
+                    const float h = r.dir.x * fx + r.dir.y * fy + r.dir.z * fz;
+                    const float c = (fx * fx + fy * fy + fz * fz) - (float)s.r2;
+                    const float disc = h * h - fa * c;
+                    if (disc >= 0) {
+                        const float sq = __builtin_sqrtf(disc), ia = __builtin_amdgcn_rcpf(fa);
+                        float ts = (h - sq) * ia;
+                        if (!(t_min < ts)) ts = (h + sq) * ia;
+                        if (t_min < ts && (double)ts < cl) {
+                            cl = ts;
+                            best = (int)asid[q];
+                        }
+                    }
+                    continue;
+                }
                 const double cx = s.cx - ox, cy = s.cy - oy, cz = s.cz - oz;
                 const double h = (dx * cx + dy * cy) + dz * cz;
                 const double c = ((cx * cx + cy * cy) + cz * cz) - s.r2;
