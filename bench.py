@@ -143,7 +143,7 @@ def main():
     for _ in range(args.warmup):
         frame()
     # one untimed instrumented frame: exact executed-work counts (sphere tests, BVH node visits)
-    pstats = torch.zeros(16, dtype=torch.int64, device=dev)
+    pstats = torch.zeros(24, dtype=torch.int64, device=dev)
     if n_rows:
         renderer.enable_profile(True)
         renderer.render_rows_async(cam.cam, out.data_ptr(), row0=row0, row_step=step, n_rows=n_rows,

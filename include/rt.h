@@ -139,12 +139,12 @@ int rt_context_kernel_times(rt_context* ctx, double* sample_ms, double* reduce_m
  * beyond that the totals restart), so a caller can time many frames without a host sync per frame.
  * *n_chunks = the number of sample-kernel launches summed. */
 int rt_context_kernel_times_total(rt_context* ctx, double* sample_ms, double* reduce_ms, uint32_t* n_chunks);
-/* Instrumented kernels (diagnostics): when enabled, `d_stats` of rt_render_rows_async must hold 16
+/* Instrumented kernels (diagnostics): when enabled, `d_stats` of rt_render_rows_async must hold 24
  * uint64: {rays, samples, sphere tests executed, BVH node visits, wave-cycles in queue refill,
  * wave-cycles in the closest-hit walk, wave-cycles in shading, wave-iterations of the BVH inner
  * (internal-node) loop, wave-iterations of BVH leaf rounds, wave-level candidate blocks (sqrt +
  * root division), wave-level second-root divisions, node visits of camera rays, sphere tests of
- * camera rays, 0...}.  Counts 0-3 are exact and
+ * camera rays, [13..15] kernel timeline stamps, [16] wave-cycles in the rejection-trip loop, 0...}.  Counts 0-3 are exact and
  * deterministic; the cycles and wave-iteration counts are diagnostics. */
 int rt_context_enable_profile(rt_context* ctx, int enable);
 

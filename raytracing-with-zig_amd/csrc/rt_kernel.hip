@@ -553,7 +553,7 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
     v3 sc_nrm = mk(0, 0, 0), sc_refl = mk(0, 0, 0);
     uint64_t rays = 0, nsamples = 0;
     Prof<kProf> pr;
-    uint64_t cyc_refill = 0, cyc_walk = 0, cyc_shade = 0;  // wave-uniform (kProf only)
+    uint64_t cyc_refill = 0, cyc_walk = 0, cyc_shade = 0, cyc_trips = 0;  // wave-uniform (kProf only)
     uint64_t rt_start = 0, rt_drain = 0;  // s_memrealtime (100 MHz) at start / first empty claim (kProf only)
     if constexpr (kProf) rt_start = __builtin_amdgcn_s_memrealtime();
 
@@ -675,7 +675,7 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
         // Lambertian and Metal scatters draw their randomUnitVec in the next iteration's trip loop
         if constexpr (kProf) {  // the trip loop counts as shading
             const uint64_t t = __builtin_amdgcn_s_memtime();
-            cyc_shade += t - t_walk0;
+            cyc_trips += t - t_walk0;
             t_walk0 = t;
         }
         if (active && !done && !pending && !dpend) {
@@ -818,6 +818,7 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
                 atomicAdd(&stats[4], (unsigned long long)cyc_refill);
                 atomicAdd(&stats[5], (unsigned long long)cyc_walk);
                 atomicAdd(&stats[6], (unsigned long long)cyc_shade);
+                atomicAdd(&stats[16], (unsigned long long)cyc_trips);
             }
         }
     }

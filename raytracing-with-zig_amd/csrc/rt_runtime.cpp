@@ -50,7 +50,7 @@ struct rt_context {
     rtk::BvhArgs bvh{};
     // optional per-kernel timing: event pairs around every sample / reduce launch of the last call
     bool timing = false;
-    bool profile = false;  // instrumented kernels: d_stats must hold 8 uint64
+    bool profile = false;  // instrumented kernels: d_stats must hold 24 uint64 (rt.h)
     int precision = RT_PRECISION_F64;
     // event pool: every timed chunk of every call takes the next 4 events (sample start/stop,
     // reduce start/stop); `call_first` / `timed_chunks` locate the last call's, `log_used` counts

@@ -32,7 +32,7 @@ r.enable_timing(True)
 row0, step, n_rows = (0, 1, H) if args.rows is None else tuple(int(x) for x in args.rows.split(":"))
 rows = dict(row0=row0, row_step=step, n_rows=n_rows)
 out = torch.empty((n_rows, W, 3), dtype=torch.float64, device="cuda:0")
-stats = torch.zeros(16, dtype=torch.int64, device="cuda:0")
+stats = torch.zeros(24, dtype=torch.int64, device="cuda:0")
 res = {"config": f"{W}x{H} {args.spp}spp, {len(cam.scene.world)} spheres", "variants": {}}
 for v in args.variants.split():
     os.environ["RTZIG_KERNEL"] = v
@@ -46,7 +46,7 @@ for v in args.variants.split():
     torch.cuda.synchronize()
     prof_ms, _ = r.kernel_times()
     s = [int(x) for x in stats.cpu().tolist()]
-    cyc = s[4] + s[5] + s[6]
+    cyc = s[4] + s[5] + s[6] + s[16]
     res["variants"][v] = {
         "kernel": r.kernel_name(), "sample_kernel_ms": round(plain_ms, 3), "instrumented_ms": round(prof_ms, 3),
         "rays": s[0], "samples": s[1], "rays_per_sample": round(s[0] / s[1], 4),
@@ -64,7 +64,7 @@ for v in args.variants.split():
                         if s[14] else None,
                         "first_drain_to_last_wave_end": round((s[15] - (~s[14] & (2**64 - 1))) / 100, 1)
                         if s[14] else None},
-        "cycle_split": {"refill": round(s[4] / cyc, 4), "walk": round(s[5] / cyc, 4), "shade": round(s[6] / cyc, 4)},
+        "cycle_split": {"refill": round(s[4] / cyc, 4), "walk": round(s[5] / cyc, 4), "shade": round(s[6] / cyc, 4), "trips": round(s[16] / cyc, 4)},
         "raw": s,
     }
     r.enable_profile(False)

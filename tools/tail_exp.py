@@ -8,7 +8,7 @@ for bm in (50, 8, 2):
         H, W = cam.height, cam.width
         r = rtzig.DeviceRenderer(0); r.set_scene(cam.scene.world); r.enable_timing(True)
         out = torch.empty((100, W, 3), dtype=torch.float64, device="cuda:0")
-        st = torch.zeros(16, dtype=torch.int64, device="cuda:0")
+        st = torch.zeros(24, dtype=torch.int64, device="cuda:0")
         ks = []
         for _ in range(4):
             r.render_rows_async(cam.cam, out.data_ptr(), row0=0, row_step=8, n_rows=100)
