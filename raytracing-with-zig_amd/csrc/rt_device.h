@@ -214,14 +214,20 @@ struct Rng {
     __device__ __forceinline__ double uniform() {
         const uint64_t rnd = next();
         const uint32_t hi = (uint32_t)(rnd >> 32);
-        if (__builtin_expect(hi < (1u << 20), 0)) return uniform_slow(rnd);
         // ohi = (hi & 0xfffff) | (1022 - lz) << 20: the exponent field e = 1022*2^20 - lz*2^20 by one
         // v_mad_i32_i24 (lz <= 11; -2^20 is a valid signed 24-bit factor), then one v_bfi_b32
         // (VOP3 takes no literals and one SGPR: the 1022 << 20 addend lives in a VGPR)
         uint32_t e, ohi;
         asm("v_mad_i32_i24 %0, %1, %2, %3" : "=v"(e) : "v"((uint32_t)__builtin_clz(hi)), "s"(-(1 << 20)), "v"(1022u << 20));
         asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(ohi) : "s"(0xfffffu), "v"(hi), "v"(e));
-        return __builtin_bit_cast(double, u32x2{(uint32_t)rnd, ohi});
+        double res = __builtin_bit_cast(double, u32x2{(uint32_t)rnd, ohi});
+        // >= 12 leading zeros (p = 2^-12 per draw): the fast result is computed for every lane and
+        // the rare lanes are redone, behind a wave-uniform test so the common case has no
+        // exec-mask branch
+        if (__builtin_expect(__ballot(hi < (1u << 20)) != 0, 0)) {
+            if (hi < (1u << 20)) res = uniform_slow(rnd);
+        }
+        return res;
     }
     __device__ __forceinline__ double uniform_slow(uint64_t rnd) {  // p = 2^-12 per draw
         uint64_t lz = rnd ? (uint64_t)__builtin_clzll(rnd) : 64;
