@@ -73,23 +73,30 @@ struct RayDiv {
     }
     __device__ __forceinline__ double div(double x) const {
         const uint32_t hi2 = (uint32_t)(__builtin_bit_cast(uint64_t, x) >> 32) << 1;
-        if (__builtin_expect(ok && hi2 - (423u << 21) < (1200u << 21), 1)) {
-            const double q0 = x * y;
-            return __builtin_fma(__builtin_fma(-a, q0, x), y, q0);
+        const double q0 = x * y;
+        double q = __builtin_fma(__builtin_fma(-a, q0, x), y, q0);
+        const bool slow = !(ok && hi2 - (423u << 21) < (1200u << 21));
+        if (__builtin_expect(__ballot(slow) != 0, 0)) {  // rare: wave-uniform test, see uniform()
+            if (slow) q = x / a;
         }
-        return x / a;
+        return q;
     }
 };
 
 // __builtin_sqrt(x) with the unscaled sequence when x is in [2^-767, inf) (the high word minus
 // that of 2^-767 is below 0x7ff00000 - 0x10000000 as an unsigned number); other lanes (0, tiny,
-// inf, NaN, negative) take the compiler's full sequence, which a wave skips when none needs it.
+// inf, NaN, negative) take the compiler's full sequence.  Every lane computes the short form, and
+// the rare lanes are redone behind a wave-uniform test, so the common case has no exec-mask branch.
 __device__ __forceinline__ bool sqrt_in_range(double x) {
     return (uint32_t)(__builtin_bit_cast(uint64_t, x) >> 32) - 0x10000000u < 0x6ff00000u;
 }
 __device__ __forceinline__ double sqrt_g(double x) {
-    if (__builtin_expect(sqrt_in_range(x), 1)) return sqrt_normal(x);
-    return __builtin_sqrt(x);
+    double r = sqrt_normal(x);
+    const bool slow = !sqrt_in_range(x);
+    if (__builtin_expect(__ballot(slow) != 0, 0)) {
+        if (slow) r = __builtin_sqrt(x);
+    }
+    return r;
 }
 
 // Vec.unit = divScalar(v, len) = v * (1/len) (vec.zig:39-45,126).  For |v|^2 in [2^-767, inf),
@@ -98,13 +105,12 @@ __device__ __forceinline__ double sqrt_g(double x) {
 // q = fma(r, y, y)) — the same bits as the correctly rounded 1.0 / len.
 __device__ __forceinline__ v3 unit(v3 a) {
     const double ls = len_sq(a);
-    double inv;
-    if (__builtin_expect(sqrt_in_range(ls), 1)) {
-        const double len = sqrt_normal(ls);
-        const double y = SharedRcp(len).y;
-        inv = __builtin_fma(__builtin_fma(-len, y, 1.0), y, y);
-    } else {
-        inv = 1.0 / __builtin_sqrt(ls);
+    const double len = sqrt_normal(ls);
+    const double y = SharedRcp(len).y;
+    double inv = __builtin_fma(__builtin_fma(-len, y, 1.0), y, y);
+    const bool slow = !sqrt_in_range(ls);
+    if (__builtin_expect(__ballot(slow) != 0, 0)) {  // rare: wave-uniform test, see sqrt_g
+        if (slow) inv = 1.0 / __builtin_sqrt(ls);
     }
     return muls(a, inv);
 }
