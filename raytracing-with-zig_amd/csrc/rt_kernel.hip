@@ -630,6 +630,7 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
         v3 col = mk(0, 0, 0);
         double ux = 0, uy = 0, uz = 0, uls = 1;
         bool got = false, dgot = false;
+#pragma unroll
         for (int trip = 0; trip < kRuvTrips; ++trip) {
             const bool wr = pending && !got, wd = dpend && !dgot;
             if (__ballot(wr || wd) == 0) break;
