@@ -561,6 +561,7 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
         uint64_t t_top = 0;
         if constexpr (kProf) t_top = __builtin_amdgcn_s_memtime();
         // ---- hand new items to lanes without a path (wave-uniform control flow) ----------------
+        bool fresh = false;
         uint64_t needy = __ballot(!active);
         while (needy != 0 && !drained) {
             if (cur >= end) {
@@ -587,29 +588,34 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
                 if (rk < take) {
                     item = cur + rk;
                     active = true;
-                    // items per launch < 2^32 (host-side chunking): 32-bit index math
-                    const uint32_t it32 = (uint32_t)item;
-                    uint32_t s_local, q;
-                    if (p.order == 0) {  // sample-major: a wave takes 64 neighbouring pixels
-                        s_local = fastdiv(it32, p.div_layer);
-                        q = it32 - s_local * P;
-                    } else {  // pixel-major: a wave takes consecutive samples of one pixel
-                        q = it32 / p.s_count;
-                        s_local = it32 - q * p.s_count;
-                    }
-                    slot = (uint64_t)s_local * P + q;
-                    const uint32_t row_local = fastdiv(q, p.div_width);
-                    const uint32_t i = q - row_local * W;
-                    const uint32_t j = p.row0 + row_local * p.row_step;
-                    const uint64_t pixel = (uint64_t)j * W + i;
-                    g.seed(sample_key(p.seed_mix, pixel, p.s_begin + s_local));
-                    dpend = camera_start(i, j, g, r);
-                    att = mk(1, 1, 1);
-                    bounce = 0;
+                    fresh = true;
                 }
             }
             cur += take;
             needy = __ballot(!active);
+        }
+        // the lanes handed an item above start their path: seeding and getRay run once, outside
+        // the claim loop, so the generator state and ray are not loop-carried through it
+        if (fresh) {
+            // items per launch < 2^32 (host-side chunking): 32-bit index math
+            const uint32_t it32 = (uint32_t)item;
+            uint32_t s_local, q;
+            if (p.order == 0) {  // sample-major: a wave takes 64 neighbouring pixels
+                s_local = fastdiv(it32, p.div_layer);
+                q = it32 - s_local * P;
+            } else {  // pixel-major: a wave takes consecutive samples of one pixel
+                q = it32 / p.s_count;
+                s_local = it32 - q * p.s_count;
+            }
+            slot = (uint64_t)s_local * P + q;
+            const uint32_t row_local = fastdiv(q, p.div_width);
+            const uint32_t i = q - row_local * W;
+            const uint32_t j = p.row0 + row_local * p.row_step;
+            const uint64_t pixel = (uint64_t)j * W + i;
+            g.seed(sample_key(p.seed_mix, pixel, p.s_begin + s_local));
+            dpend = camera_start(i, j, g, r);
+            att = mk(1, 1, 1);
+            bounce = 0;
         }
         if (__ballot(active) == 0) break;
         uint64_t t_walk0 = 0, t_walk1 = 0;

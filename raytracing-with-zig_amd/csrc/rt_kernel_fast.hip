@@ -317,7 +317,7 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
     uint64_t cur = 0, end = 0, last_chunk = 0;
     bool drained = false;
     bool active = false, pending = false, sc_metal = false, dpend = false;
-    uint64_t slot = 0;
+    uint64_t item = 0, slot = 0;
     Rng g;
     Ray r;
     f3 att = mk(1, 1, 1), sc_nrm = mk(0, 0, 0), sc_refl = mk(0, 0, 0);
@@ -327,6 +327,7 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
 
     while (true) {
         // ---- refill (as the parity kernel's path_loop) -----------------------------------------
+        bool fresh = false;
         uint64_t needy = __ballot(!active);
         while (needy != 0 && !drained) {
             if (cur >= end) {
@@ -350,28 +351,34 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
             if (!active) {
                 const uint32_t rk = rank_in(needy);
                 if (rk < take) {
+                    item = cur + rk;
                     active = true;
-                    const uint32_t it32 = (uint32_t)(cur + rk);
-                    uint32_t s_local, q;
-                    if (p.order == 0) {  // sample-major: a wave takes 64 neighbouring pixels
-                        s_local = rtk::fastdiv(it32, p.div_layer);
-                        q = it32 - s_local * P;
-                    } else {
-                        q = it32 / p.s_count;
-                        s_local = it32 - q * p.s_count;
-                    }
-                    slot = (uint64_t)s_local * P + q;
-                    const uint32_t row_local = rtk::fastdiv(q, p.div_width);
-                    const uint32_t i = q - row_local * W;
-                    const uint32_t j = p.row0 + row_local * p.row_step;
-                    g.seed(rtk::sample_key(p.seed_mix, (uint64_t)j * W + i, p.s_begin + s_local));
-                    dpend = camera_start(i, j, g, r);
-                    att = mk(1, 1, 1);
-                    bounce = 0;
+                    fresh = true;
                 }
             }
             cur += take;
             needy = __ballot(!active);
+        }
+        // the lanes handed an item above start their path: seeding and getRay run once, outside
+        // the claim loop, so the generator state and ray are not loop-carried through it
+        if (fresh) {
+            const uint32_t it32 = (uint32_t)item;
+            uint32_t s_local, q;
+            if (p.order == 0) {  // sample-major: a wave takes 64 neighbouring pixels
+                s_local = rtk::fastdiv(it32, p.div_layer);
+                q = it32 - s_local * P;
+            } else {
+                q = it32 / p.s_count;
+                s_local = it32 - q * p.s_count;
+            }
+            slot = (uint64_t)s_local * P + q;
+            const uint32_t row_local = rtk::fastdiv(q, p.div_width);
+            const uint32_t i = q - row_local * W;
+            const uint32_t j = p.row0 + row_local * p.row_step;
+            g.seed(rtk::sample_key(p.seed_mix, (uint64_t)j * W + i, p.s_begin + s_local));
+            dpend = camera_start(i, j, g, r);
+            att = mk(1, 1, 1);
+            bounce = 0;
         }
         if (__ballot(active) == 0) break;
 
