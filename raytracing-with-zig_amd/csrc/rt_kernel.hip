@@ -314,7 +314,11 @@ struct BvhWalker {
     template <class PR>
     __device__ __forceinline__ void test_always(uint32_t q, const Ray& r, double a, const RayDiv& ad, double t_min, const LeafFilter& lfilt,
                                                 double& closest, uint32_t& best, bool& found, PR& pr) const {
-        const GeoRec s = ageo[q];
+        // uniform address, read-only data: one scalar load (the compiler emits per-lane vector
+        // loads, since it cannot prove the kernel's stores do not alias it)
+        u32x8 w;
+        asm volatile("s_load_dwordx8 %0, %1, 0\n\ts_waitcnt lgkmcnt(0)" : "=s"(w) : "s"(ageo + q));
+        const GeoRec s{dw2d(w[0], w[1]), dw2d(w[2], w[3]), dw2d(w[4], w[5]), dw2d(w[6], w[7])};
         const double ocx = s.cx - r.orig.x;
         const double ocy = s.cy - r.orig.y;
         const double ocz = s.cz - r.orig.z;
@@ -360,7 +364,15 @@ struct BvhWalker {
         bool found = false;
         const LeafFilter lfilt = LeafFilter::make(a, t_min);
         const RayDiv ad(a);
-        for (uint32_t q = 0; q < n_always; ++q) test_always(q, r, a, ad, t_min, lfilt, closest, best, found, pr);
+        if (n_always <= 4) {
+            // the common case (the ground and up to three big spheres), unrolled so that closest /
+            // best / found are not loop-carried through a runtime-bounded loop
+#pragma unroll
+            for (uint32_t q = 0; q < 4; ++q)
+                if (q < n_always) test_always(q, r, a, ad, t_min, lfilt, closest, best, found, pr);
+        } else {
+            for (uint32_t q = 0; q < n_always; ++q) test_always(q, r, a, ad, t_min, lfilt, closest, best, found, pr);
+        }
         pr.tests(n_always);
 
         // f32 ray for the conservative slab tests (error budget: rt_bvh.cpp)
