@@ -66,20 +66,26 @@ struct SharedRcp {
 // lanes take the compiler's full division.
 struct RayDiv {
     double a, y;
-    bool ok;
+    uint64_t bad;  // wave mask of the lanes whose `a` is out of range (a ballot: one SGPR pair)
     __device__ __forceinline__ explicit RayDiv(double den) : a(den) {
-        ok = den >= 0x1p-100 && den <= 0x1p100;
+        bad = __ballot(!(den >= 0x1p-100 && den <= 0x1p100));
         y = SharedRcp(den).y;
     }
     __device__ __forceinline__ double div(double x) const {
         const uint32_t hi2 = (uint32_t)(__builtin_bit_cast(uint64_t, x) >> 32) << 1;
         const double q0 = x * y;
         double q = __builtin_fma(__builtin_fma(-a, q0, x), y, q0);
-        const bool slow = !(ok && hi2 - (423u << 21) < (1200u << 21));
-        if (__builtin_expect(__ballot(slow) != 0, 0)) {  // rare: wave-uniform test, see uniform()
-            if (slow) q = x / a;
+        const bool far = !(hi2 - (423u << 21) < (1200u << 21));
+        // rare: wave-uniform test, see uniform().  The per-ray part is the mask `bad`, OR-ed on the
+        // scalar unit; folding it into the per-lane bool made the compiler materialize that bool
+        // with two VALU ops per division.
+        if (__builtin_expect((__ballot(far) | bad) != 0, 0)) {
+            if (far || ((bad >> lane()) & 1)) q = x / a;
         }
         return q;
+    }
+    __device__ __forceinline__ static uint32_t lane() {
+        return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
     }
 };
 

@@ -481,6 +481,20 @@ struct BvhWalker {
                 // win (LeafFilter) and then feeds its viable slots through ONE block per round,
                 // nearest-looking (smallest h) first; a second round runs only for lanes with a
                 // second slot still viable after `closest` has shrunk.
+                if constexpr (kLeafBvh == 2 && RTZIG_LEAF_FILTER == 1) {
+                    // the same rounds written out for two slots, so the viability flags stay lane
+                    // masks (the generic form keeps them as 0/1 VGPRs and re-compares them)
+                    const bool v0 = disc[0] >= 0 && !lfilt.behind(h[0], disc[0]);
+                    const bool v1 = disc[1] >= 0 && !lfilt.behind(h[1], disc[1]);
+                    const bool p1 = v1 && (!v0 || h[1] < h[0]);  // round 1 takes slot 1
+                    const uint32_t s0 = lf->sid[0], s1 = lf->sid[1];
+                    if (v0 || v1)
+                        candidate(p1 ? s1 : s0, p1 ? h[1] : h[0], p1 ? disc[1] : disc[0], ad, t_min, closest, best,
+                                  found, pr);
+                    if (v0 && v1)  // round 2: the other slot
+                        candidate(p1 ? s0 : s1, p1 ? h[0] : h[1], p1 ? disc[0] : disc[1], ad, t_min, closest, best,
+                                  found, pr);
+                } else {
                 bool v[kLeafBvh];
                 uint32_t sid[kLeafBvh];
 #pragma unroll
@@ -517,6 +531,7 @@ struct BvhWalker {
 #endif
                         }
                     }
+                }
                 }
 #endif
                 pr.tests(kLeafBvh);
