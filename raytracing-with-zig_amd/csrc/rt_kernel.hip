@@ -241,6 +241,13 @@ __device__ __forceinline__ float slab_far(float x, float y, float z, float upper
     return r;
 }
 
+// v_cndmask_b32 on a wave mask held in SGPRs: lanes whose bit of `m` is set get `t`, others `f`
+__device__ __forceinline__ int32_t sel_mask(int32_t f, int32_t t, uint64_t m) {
+    int32_t r;
+    asm("v_cndmask_b32 %0, %1, %2, %3" : "=v"(r) : "v"(f), "v"(t), "s"(m));
+    return r;
+}
+
 // BVH walk (rt_bvh.hpp): per-lane, near-child-first, stack in LDS.  Every visited sphere runs the
 // same f64 quadratic as the linear walk; the candidate root of sphere k is
 //   t_k = root1 if t_min < root1, else root2 if t_min < root2   (sphere.zig:38-41),
@@ -444,15 +451,18 @@ struct BvhWalker {
                 const f2 tz1 = __builtin_elementwise_fma(bz1, inv_z, noi_z);
                 const float n0 = slab_near(tx0.x, ty0.x, tz0.x, lower), f0 = slab_far(tx0.y, ty0.y, tz0.y, upper);
                 const float n1 = slab_near(tx1.x, ty1.x, tz1.x, lower), f1 = slab_far(tx1.y, ty1.y, tz1.y, upper);
-                const bool h0 = n0 <= f0;
-                const bool h1 = n1 <= f1;
                 // both hit: descend into the nearer child and push the farther one (the store
-                // always happens; it only counts when sp advances); one hit: descend; none: pop
-                const bool first0 = n0 <= n1;
-                top[kBlockBvh] = first0 ? ref1 : ref0;
-                const bool pick0 = h0 && (!h1 || first0);  // both: nearer; one: that one
-                cur = (h0 || h1) ? (pick0 ? ref0 : ref1) : popped;
-                top += (h0 && h1) ? kBlockBvh : ((h0 || h1) ? 0 : -kBlockBvh);
+                // always happens; it only counts when sp advances); one hit: descend; none: pop.
+                // The three compares are taken as wave masks and combined on the scalar unit, and
+                // the selects are v_cndmask on those masks: 3 compares + 5 selects (the compiler's
+                // form of the same logic re-compared a negated mask on the VALU).
+                const uint64_t m0 = __ballot(n0 <= f0), m1 = __ballot(n1 <= f1), mf = __ballot(n0 <= n1);
+                const uint64_t pick0 = m0 & (~m1 | mf);  // both: nearer; one: that one
+                const uint64_t any = m0 | m1, both = m0 & m1;
+                const int32_t near = sel_mask(ref1, ref0, pick0), far = sel_mask(ref0, ref1, pick0);
+                top[kBlockBvh] = far;
+                cur = sel_mask(popped, near, any);
+                top += sel_mask(sel_mask(-kBlockBvh, 0, any), kBlockBvh, both);
             }
             if (cur != kDone) {
                 pr.leaf_iter();
