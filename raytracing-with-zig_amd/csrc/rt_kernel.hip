@@ -317,14 +317,48 @@ struct BvhWalker {
     uint32_t n_always;
     int32_t* stack;                      // LDS, element i of this lane at stack[i * kBlockBvh]
 
-    // always-list sphere q
+    // always-list sphere q: geometry + original index from global memory (uniform address,
+    // read-only data: scalar loads; the compiler emits per-lane vector loads, since it cannot prove
+    // the kernel's stores do not alias it)
     template <class PR>
     __device__ __forceinline__ void test_always(uint32_t q, const Ray& r, double a, const RayDiv& ad, double t_min, const LeafFilter& lfilt,
                                                 double& closest, uint32_t& best, bool& found, PR& pr) const {
-        // uniform address, read-only data: one scalar load (the compiler emits per-lane vector
-        // loads, since it cannot prove the kernel's stores do not alias it)
         u32x8 w;
         asm volatile("s_load_dwordx8 %0, %1, 0\n\ts_waitcnt lgkmcnt(0)" : "=s"(w) : "s"(ageo + q));
+        test_always_geo(w, asid[q], r, a, ad, t_min, lfilt, closest, best, found, pr);
+    }
+    // the same for a compile-time Q < 4 (the unrolled common case): the always-list pointers are
+    // re-read from the kernarg segment (BvhArgs, the kernel's second argument) and the sphere sits
+    // at an immediate offset, so no per-sphere address is held in SGPRs across the walk (held,
+    // they were spilled to VGPR lanes and reloaded with v_readlane)
+    template <int Q, class PR>
+    __device__ __forceinline__ void test_always_c(const Ray& r, double a, const RayDiv& ad, double t_min, const LeafFilter& lfilt,
+                                                  double& closest, uint32_t& best, bool& found, PR& pr) const {
+        static_assert(sizeof(KernelParams) == 336 && offsetof(BvhArgs, always_geo) == 16 &&
+                          offsetof(BvhArgs, always_sid) == 24,
+                      "kernarg offsets of BvhArgs::always_geo / always_sid");
+        constexpr int kGeoPtr = 336 + 16, kSidPtr = 336 + 24;
+        const uint64_t kp = (uint64_t)__builtin_amdgcn_kernarg_segment_ptr();
+        uint64_t pg, ps;
+        asm volatile("s_load_dwordx2 %0, %2, %3\n\ts_load_dwordx2 %1, %2, %4\n\ts_waitcnt lgkmcnt(0)"
+                     : "=s"(pg), "=s"(ps) : "s"(kp), "i"(kGeoPtr), "i"(kSidPtr));
+        u32x8 w;
+        uint32_t sid;
+        asm volatile("s_load_dwordx8 %0, %2, %3\n\ts_load_dword %1, %4, %5\n\ts_waitcnt lgkmcnt(0)"
+                     : "=s"(w), "=s"(sid) : "s"(pg), "i"(Q * 32), "s"(ps), "i"(Q * 4));
+        test_always_geo(w, sid, r, a, ad, t_min, lfilt, closest, best, found, pr);
+    }
+    __device__ __forceinline__ static uint32_t n_always_now() {
+        static_assert(offsetof(BvhArgs, n_always) == 40, "kernarg offset of BvhArgs::n_always");
+        const uint64_t kp = (uint64_t)__builtin_amdgcn_kernarg_segment_ptr();
+        uint32_t n;
+        asm volatile("s_load_dword %0, %1, %2\n\ts_waitcnt lgkmcnt(0)" : "=s"(n) : "s"(kp), "i"(336 + 40));
+        return n;
+    }
+    template <class PR>
+    __device__ __forceinline__ static void test_always_geo(const u32x8& w, uint32_t sid, const Ray& r, double a, const RayDiv& ad,
+                                                           double t_min, const LeafFilter& lfilt, double& closest,
+                                                           uint32_t& best, bool& found, PR& pr) {
         const GeoRec s{dw2d(w[0], w[1]), dw2d(w[2], w[3]), dw2d(w[4], w[5]), dw2d(w[6], w[7])};
         const double ocx = s.cx - r.orig.x;
         const double ocy = s.cy - r.orig.y;
@@ -333,10 +367,10 @@ struct BvhWalker {
         const double c = ((ocx * ocx + ocy * ocy) + ocz * ocz) - s.r2;
         const double disc = h * h - a * c;
 #if RTZIG_LEAF_FILTER == 0
-        if (disc >= 0) candidate(asid[q], h, disc, ad, t_min, closest, best, found, pr);
+        if (disc >= 0) candidate(sid, h, disc, ad, t_min, closest, best, found, pr);
 #else
         // the ground sphere is "behind" every ray that leaves it: no sqrt / second-root division
-        if (disc >= 0 && !lfilt.behind(h, disc)) candidate(asid[q], h, disc, ad, t_min, closest, best, found, pr);
+        if (disc >= 0 && !lfilt.behind(h, disc)) candidate(sid, h, disc, ad, t_min, closest, best, found, pr);
 #endif
     }
 
@@ -374,9 +408,12 @@ struct BvhWalker {
         if (n_always <= 4) {
             // the common case (the ground and up to three big spheres), unrolled so that closest /
             // best / found are not loop-carried through a runtime-bounded loop
-#pragma unroll
-            for (uint32_t q = 0; q < 4; ++q)
-                if (q < n_always) test_always(q, r, a, ad, t_min, lfilt, closest, best, found, pr);
+            // n_always is re-read from the kernarg segment at each test (a held copy of each
+            // `n_always > q` was kept as a spilled lane mask)
+            if (n_always_now() > 0) test_always_c<0>(r, a, ad, t_min, lfilt, closest, best, found, pr);
+            if (n_always_now() > 1) test_always_c<1>(r, a, ad, t_min, lfilt, closest, best, found, pr);
+            if (n_always_now() > 2) test_always_c<2>(r, a, ad, t_min, lfilt, closest, best, found, pr);
+            if (n_always_now() > 3) test_always_c<3>(r, a, ad, t_min, lfilt, closest, best, found, pr);
         } else {
             for (uint32_t q = 0; q < n_always; ++q) test_always(q, r, a, ad, t_min, lfilt, closest, best, found, pr);
         }
