@@ -15,6 +15,9 @@ constexpr uint32_t kPad = 4;               // sphere list padded to a multiple o
 #ifndef RTZIG_RUV_TRIPS
 #define RTZIG_RUV_TRIPS 3
 #endif
+#ifndef RTZIG_TRIP_DEFER
+#define RTZIG_TRIP_DEFER 0  // >0: skip trips 2.. when at most this many lanes still need a draw
+#endif
 constexpr int kRuvTrips = RTZIG_RUV_TRIPS;  // randomUnitVec rejection trips per loop iteration (path_loop)
 constexpr const char* kDefaultVariant = "smem_u4";  // see variant_choice() in rt_kernel.hip
 

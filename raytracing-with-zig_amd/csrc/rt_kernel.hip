@@ -713,7 +713,13 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
 #pragma unroll
         for (int trip = 0; trip < kRuvTrips; ++trip) {
             const bool wr = pending && !got, wd = dpend && !dgot;
-            if (__ballot(wr || wd) == 0) break;
+            const uint64_t need = __ballot(wr || wd);
+            if (need == 0) break;
+#if RTZIG_TRIP_DEFER > 0
+            // a late trip that only a few lanes need is left to the next iteration (those lanes stay
+            // pending and skip one walk) instead of costing the whole wave a trip now
+            if (trip > 0 && __popcll(need) <= RTZIG_TRIP_DEFER) break;
+#endif
             if (wr || wd) {
                 ux = g.range_pm1();
                 uy = g.range_pm1();
