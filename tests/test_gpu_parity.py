@@ -364,3 +364,39 @@ def test_sample_chunked_workspace_bit_exact(oracle, monkeypatch, mb):
     assert np.array_equal(out, ref) and st["rays"] == rays and st["samples"] == 400 * 225 * 7
     rgb, _ = gpu_render(cam, cam.scene.world, n_gpus=1, output="rgb8")
     assert np.array_equal(rgb, oracle.to_rgb8(ref))
+
+
+@pytest.mark.parametrize("n_big,ground,n_unbound", [(0, False, 0), (0, True, 0), (1, True, 0), (2, True, 0),
+                                                    (3, True, 0), (4, True, 0), (3, True, 2)])
+def test_always_list_sizes_bit_exact(oracle, n_big, ground, n_unbound):
+    """The always-list (rt_bvh.cpp: huge / big / unboundable spheres tested by every ray before the
+    walk) at every size the kernel distinguishes: 0 to 4 spheres take the unrolled path whose
+    geometry and original index come by scalar loads at immediate offsets from the kernarg
+    pointers; more than 4 (unboundable spheres beside the capped big ones) take the runtime loop.
+    A grid of small spheres with n_big radius-1.2 spheres among them (box area >= 10x the median:
+    big), an optional radius-1000 ground (huge) and n_unbound spheres centred at 2e30 (never hit,
+    but tested)."""
+    rng = np.random.default_rng(100 + 10 * n_big + n_unbound + (5 if ground else 0))
+    sph = []
+    for a in range(-4, 4):
+        for b in range(-4, 4):
+            sph.append(RtSphere(center=D3(a + 0.9 * rng.uniform(), 0.2, b + 0.9 * rng.uniform()), radius=0.2,
+                                material=int(rng.integers(0, 3)), albedo=D3(*rng.uniform(0, 1, 3)),
+                                fuzz=float(rng.uniform(0, 0.5)), refraction_index=1.5))
+    for k in range(n_big):
+        sph.append(RtSphere(center=D3(-3.0 + 2.0 * k, 1.2, 0.3 * k), radius=1.2, material=k % 3,
+                            albedo=D3(0.7, 0.6, 0.5), fuzz=0.0, refraction_index=1.5))
+    if ground:
+        sph.insert(int(rng.integers(0, len(sph))), RtSphere(center=D3(0, -1000, 0), radius=1000.0, material=0,
+                                                            albedo=D3(0.5, 0.5, 0.5)))
+    for k in range(n_unbound):
+        sph.insert(int(rng.integers(0, len(sph))), RtSphere(center=D3(2e30, 1.0 + k, 0), radius=1.0, material=0,
+                                                            albedo=D3(0.5, 0.5, 0.5)))
+    arr = (RtSphere * len(sph))(*sph)
+    scene = rtzig.Scene.init(7)
+    scene.world = arr
+    cam = (rtzig.Camera.builder(64, 1.5).setScene(scene).setDefocusAngle(0.6).setFocusDist(10.0)
+           .setViewport((13, 2, 3), (0, 0, 0), 20.0).setSamplesPerPixel(4).build())
+    out, st = gpu_render(cam, arr, n_gpus=1)
+    ref, rays = oracle.render_b(cam.cam, arr, threads=8)
+    assert np.array_equal(out, ref) and st["rays"] == rays
