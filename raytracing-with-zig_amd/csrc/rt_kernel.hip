@@ -421,18 +421,22 @@ struct BvhWalker {
 
         // f32 ray for the conservative slab tests (error budget: rt_bvh.cpp)
         const float ox = (float)r.orig.x, oy = (float)r.orig.y, oz = (float)r.orig.z;
-        float dx = (float)r.dir.x, dy = (float)r.dir.y, dz = (float)r.dir.z;
-        if (__builtin_fabsf(dx) < 1e-30f) dx = __builtin_copysignf(1e-30f, dx);
-        if (__builtin_fabsf(dy) < 1e-30f) dy = __builtin_copysignf(1e-30f, dy);
-        if (__builtin_fabsf(dz) < 1e-30f) dz = __builtin_copysignf(1e-30f, dz);
-        // v_rcp_f32 (1 ulp) instead of three correctly rounded f32 divisions (~11 ops each)
-        const float ix = __builtin_amdgcn_rcpf(dx), iy = __builtin_amdgcn_rcpf(dy), iz = __builtin_amdgcn_rcpf(dz);
+        const float dx = (float)r.dir.x, dy = (float)r.dir.y, dz = (float)r.dir.z;
+        // v_rcp_f32 (1 ulp) instead of three correctly rounded f32 divisions (~11 ops each), then
+        // clamped to +-1e30 by one v_med3 per axis: the inverse of a component clamped to
+        // +-1e-30 (rcp(+-0) = +-inf keeps its sign), one op instead of compare + copysign + select
+        const float ix = __builtin_amdgcn_fmed3f(__builtin_amdgcn_rcpf(dx), -1e30f, 1e30f);
+        const float iy = __builtin_amdgcn_fmed3f(__builtin_amdgcn_rcpf(dy), -1e30f, 1e30f);
+        const float iz = __builtin_amdgcn_fmed3f(__builtin_amdgcn_rcpf(dz), -1e30f, 1e30f);
         // slab planes as t = fma(bound, inv, -o*inv): one op per plane.  Error (position space,
         // per axis) <= 2^-24 (4|bound| + 5|o|), inside the padding of rt_bvh.cpp.  fma is monotone
         // in `bound`, so for inv > 0 the lo plane is the near one and for inv < 0 the hi plane: the
         // lane reads its (near, far) pair per axis at byte +0 or +8 of the axis's {lo, hi, hi, lo}
-        // (rtk::BvhNode) and both planes of an axis come out of one packed fma.  inv is never 0 or
-        // NaN (|d| >= 1e-30), so the pick matches the min/max of the two planes exactly; an
+        // (rtk::BvhNode) and both planes of an axis come out of one packed fma.  inv is finite, and
+        // nonzero unless the f32 component overflowed (then every point of the ray past t_min lies
+        // beyond any boundable box, and the [0, 0] slab culls it correctly), and NaN only for a NaN
+        // direction (whose f64 sphere tests never pass), so the pick matches the min/max of the
+        // two planes exactly; an
         // overflowed plane is +-inf in ray order, and NaN arises only from a NaN origin, which
         // v_max3/v_min3 drop (the box is kept: permissive, never a wrong cull).
         const uint32_t ax = ix < 0 ? 8u : 0u, ay = 16u + (iy < 0 ? 8u : 0u), az = 32u + (iz < 0 ? 8u : 0u);
