@@ -254,6 +254,13 @@ __device__ __forceinline__ int32_t sel_mask(int32_t f, int32_t t, uint64_t m) {
 // and it wins iff t_k < closest, or t_k == closest and k is lower (the linear scan's first-wins).
 constexpr int32_t kDone = INT32_MIN;  // walk finished (stack entry 0)
 typedef float f2 __attribute__((ext_vector_type(2)));
+// {b.x * m.x + a.x, b.y * m.x + a.x}: v_pk_fma_f32 with the second and third operands' low halves
+// broadcast to the high lane (op_sel_hi:[1,0,0]); their high halves are never read
+__device__ __forceinline__ f2 pk_fma_lo(f2 b, f2 m, f2 a) {
+    f2 r;
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[1,0,0]" : "=v"(r) : "v"(b), "v"(m), "v"(a));
+    return r;
+}
 typedef int32_t i2 __attribute__((ext_vector_type(2)));
 
 // LDS reads issued as single instructions (the caller waits with s_waitcnt lgkmcnt(0), naming the
@@ -440,8 +447,11 @@ struct BvhWalker {
         // overflowed plane is +-inf in ray order, and NaN arises only from a NaN origin, which
         // v_max3/v_min3 drop (the box is kept: permissive, never a wrong cull).
         const uint32_t ax = ix < 0 ? 8u : 0u, ay = 16u + (iy < 0 ? 8u : 0u), az = 32u + (iz < 0 ? 8u : 0u);
-        const f2 inv_x = {ix, ix}, inv_y = {iy, iy}, inv_z = {iz, iz};
-        const f2 noi_x = {-(ox * ix), -(ox * ix)}, noi_y = {-(oy * iy), -(oy * iy)}, noi_z = {-(oz * iz), -(oz * iz)};
+        // per-axis constants live in the low half of a register pair; pk_fma_lo broadcasts them to
+        // both lanes of the packed fma (op_sel_hi), so they are not duplicated with v_mov
+        f2 inv_x, inv_y, inv_z, noi_x, noi_y, noi_z;
+        inv_x.x = ix; inv_y.x = iy; inv_z.x = iz;
+        noi_x.x = -(ox * ix); noi_y.x = -(oy * iy); noi_z.x = -(oz * iz);
         float lower = (float)t_min;
         lower = lower - __builtin_fabsf(lower) * 0x1p-20f - 1e-30f;
         float upper = (float)closest;
@@ -484,12 +494,12 @@ struct BvhWalker {
                     ref1 = *(const int32_t*)(nb + 100);
                     popped = *top;
                 }
-                const f2 tx0 = __builtin_elementwise_fma(bx0, inv_x, noi_x);
-                const f2 ty0 = __builtin_elementwise_fma(by0, inv_y, noi_y);
-                const f2 tz0 = __builtin_elementwise_fma(bz0, inv_z, noi_z);
-                const f2 tx1 = __builtin_elementwise_fma(bx1, inv_x, noi_x);
-                const f2 ty1 = __builtin_elementwise_fma(by1, inv_y, noi_y);
-                const f2 tz1 = __builtin_elementwise_fma(bz1, inv_z, noi_z);
+                const f2 tx0 = pk_fma_lo(bx0, inv_x, noi_x);
+                const f2 ty0 = pk_fma_lo(by0, inv_y, noi_y);
+                const f2 tz0 = pk_fma_lo(bz0, inv_z, noi_z);
+                const f2 tx1 = pk_fma_lo(bx1, inv_x, noi_x);
+                const f2 ty1 = pk_fma_lo(by1, inv_y, noi_y);
+                const f2 tz1 = pk_fma_lo(bz1, inv_z, noi_z);
                 const float n0 = slab_near(tx0.x, ty0.x, tz0.x, lower), f0 = slab_far(tx0.y, ty0.y, tz0.y, upper);
                 const float n1 = slab_near(tx1.x, ty1.x, tz1.x, lower), f1 = slab_far(tx1.y, ty1.y, tz1.y, upper);
                 // both hit: descend into the nearer child and push the farther one (the store
