@@ -796,20 +796,33 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
                 // dielectric (unit(ray.dir)) and the metal (unit(reflect(ray.dir, n))).  Each is a
                 // correctly rounded sqrt and division, and a wave executes every branch some lane
                 // takes; so each lane selects its vector first and one unit() serves all three.
-                GeoRec sg{};
-                MatRec m{};
-                v3 pt = mk(0, 0, 0), nrm = mk(0, 0, 0);
-                bool front = false;
+                // The hit record and material are read only by lanes with a hit (k >= 0).  They start
+                // as arbitrary values (__builtin_nondeterministic_value: no instruction), not zeros:
+                // zero-initialized, they cost ~15 v_mov per iteration for the sky lanes.
+                v3 pt = mk(__builtin_nondeterministic_value(0.0), __builtin_nondeterministic_value(0.0),
+                           __builtin_nondeterministic_value(0.0));
+                v3 nrm = mk(__builtin_nondeterministic_value(0.0), __builtin_nondeterministic_value(0.0),
+                            __builtin_nondeterministic_value(0.0));
+                v3 alb = mk(__builtin_nondeterministic_value(0.0), __builtin_nondeterministic_value(0.0),
+                            __builtin_nondeterministic_value(0.0));
+                double fuzz = __builtin_nondeterministic_value(0.0), ri = __builtin_nondeterministic_value(0.0),
+                       r0 = __builtin_nondeterministic_value(0.0);
+                uint32_t kind = __builtin_nondeterministic_value(0u);
                 v3 x = r.dir;
                 if (k >= 0) {
-                    sg = geo_orig[k];
-                    m = mat_g[k];
+                    const GeoRec sg = geo_orig[k];
+                    const MatRec m = mat_g[k];
                     // hit record (sphere.zig:44-53)
                     pt = r.orig + muls(r.dir, t);
                     const v3 outward = muls(pt - mk(sg.cx, sg.cy, sg.cz), m.inv_r);
-                    front = dot(r.dir, outward) < 0;
+                    const bool front = dot(r.dir, outward) < 0;
                     nrm = front ? outward : -outward;
-                    if (m.kind == 1) x = reflect(r.dir, nrm);
+                    kind = m.kind;
+                    alb = mk(m.albedo[0], m.albedo[1], m.albedo[2]);
+                    fuzz = m.fuzz;
+                    ri = front ? m.inv_ior : m.ior;        // dielectric: 1.0 / ior precomputed (same bits)
+                    r0 = front ? m.r0_front : m.r0_back;   // Schlick ((1-ri)/(1+ri))^2, host
+                    if (kind == 1) x = reflect(r.dir, nrm);
                 }
                 const v3 u = unit(x);
                 if (k < 0) {
@@ -818,24 +831,22 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
                     const v3 sky = muls(mk(1, 1, 1), 1.0 - a) + muls(mk(0.5, 0.7, 1), a);
                     col = att * sky;
                     done = true;
-                } else if (m.kind <= 1) {
+                } else if (kind <= 1) {
                     // Lambertian (material.zig:27-39) / Metal (:55-68): attenuation = albedo.  A
                     // metal ray that ends up absorbed returns black whatever `att` is, so the
                     // product can be taken now.
-                    att = att * mk(m.albedo[0], m.albedo[1], m.albedo[2]);
+                    att = att * alb;
                     pending = true;
-                    sc_metal = m.kind == 1;
-                    sc_fuzz = m.fuzz;
+                    sc_metal = kind == 1;
+                    sc_fuzz = fuzz;
                     sc_nrm = nrm;
                     sc_refl = u;
                     r.orig = pt;
                 } else {  // Dielectric.scatter (material.zig:82-110), attenuation (1,1,1)
-                    const double ri = front ? m.inv_ior : m.ior;  // 1.0 / ior precomputed (same bits)
                     const v3 ud = u;
                     const double cos_t = __builtin_fmin(dot(-ud, nrm), 1.0);
                     const double sin_t = sqrt_g(1.0 - cos_t * cos_t);
                     const bool cannot = ri * sin_t > 1.0;
-                    const double r0 = front ? m.r0_front : m.r0_back;  // ((1-ri)/(1+ri))^2, host
                     const double approx = r0 + (1 - r0) * zig_pow5(1 - cos_t);
                     // short-circuit `or` (material.zig:94): draw only if refraction is possible
                     const v3 dir = (cannot || approx > g.uniform()) ? reflect(ud, nrm) : refract(ud, nrm, ri);
