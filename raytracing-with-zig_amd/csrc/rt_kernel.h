@@ -10,7 +10,10 @@ namespace rtk {
 
 constexpr int kBlock = 256;                // 4 waves of 64 lanes
 constexpr uint32_t kMaxLdsSpheres = 2048;  // 64 KiB of LDS geometry; above this, read from global
-constexpr uint32_t kChunk = 2048;          // work items a wave claims per queue fetch (at most: guided_chunk)
+#ifndef RTZIG_CHUNK
+#define RTZIG_CHUNK 2048
+#endif
+constexpr uint32_t kChunk = RTZIG_CHUNK;          // work items a wave claims per queue fetch (at most: guided_chunk)
 constexpr uint32_t kPad = 4;               // sphere list padded to a multiple of this (sentinels)
 #ifndef RTZIG_RUV_TRIPS
 #define RTZIG_RUV_TRIPS 3

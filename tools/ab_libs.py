@@ -25,12 +25,15 @@ ap.add_argument("--width", type=int, default=1200)
 ap.add_argument("--aspect", type=float, default=1.5)
 ap.add_argument("--spp", type=int, default=100)
 ap.add_argument("--rounds", type=int, default=5)
+ap.add_argument("--row-step", type=int, default=1,
+                help="render rank 0's interleaved row set of an N-rank job (rows 0, N, 2N, ...)")
 ap.add_argument("--no-check", action="store_true", help="ablation builds: skip the bit-equality check")
 args = ap.parse_args()
 
 cam = rtzig.final_scene_camera(width=args.width, aspect_ratio=args.aspect, spp=args.spp)
 H, W = cam.height, cam.width
-out = torch.empty((H, W, 3), dtype=torch.float64, device="cuda:0")
+NR = (H + args.row_step - 1) // args.row_step
+out = torch.empty((NR, W, 3), dtype=torch.float64, device="cuda:0")
 runs = []
 for path in args.libs:
     L = C.CDLL(os.path.abspath(path))
@@ -53,7 +56,7 @@ times = {p: [] for p, _, _ in runs}
 ref = None
 for rnd in range(args.rounds + 1):
     for path, L, ctx in runs:
-        rc = L.rt_render_rows_async(ctx, C.byref(cam.cam), 0, 0, 1, H, C.c_void_p(out.data_ptr()), None, None)
+        rc = L.rt_render_rows_async(ctx, C.byref(cam.cam), 0, 0, args.row_step, NR, C.c_void_p(out.data_ptr()), None, None)
         assert rc == 0, L.rt_last_error()
         torch.cuda.synchronize()
         a, b = C.c_double(), C.c_double()
@@ -66,5 +69,5 @@ for rnd in range(args.rounds + 1):
         if rnd > 0:
             times[path].append(a.value)
 res = {p: {"median_ms": round(statistics.median(t), 3), "min_ms": round(min(t), 3),
-           "Msamples_s": round(W * H * args.spp / statistics.median(t) / 1e3, 1)} for p, t in times.items()}
-print(json.dumps({"config": f"{W}x{H} {args.spp}spp", "results": res}))
+           "Msamples_s": round(W * NR * args.spp / statistics.median(t) / 1e3, 1)} for p, t in times.items()}
+print(json.dumps({"config": f"{W}x{H} {args.spp}spp rows 0::{args.row_step}", "results": res}))
