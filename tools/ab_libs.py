@@ -25,12 +25,18 @@ ap.add_argument("--width", type=int, default=1200)
 ap.add_argument("--aspect", type=float, default=1.5)
 ap.add_argument("--spp", type=int, default=100)
 ap.add_argument("--rounds", type=int, default=5)
+ap.add_argument("--scene", choices=["final", "ch13", "ch9"], default="final")
 ap.add_argument("--row-step", type=int, default=1,
                 help="render rank 0's interleaved row set of an N-rank job (rows 0, N, 2N, ...)")
 ap.add_argument("--no-check", action="store_true", help="ablation builds: skip the bit-equality check")
 args = ap.parse_args()
 
-cam = rtzig.final_scene_camera(width=args.width, aspect_ratio=args.aspect, spp=args.spp)
+if args.scene == "final":
+    cam = rtzig.final_scene_camera(width=args.width, aspect_ratio=args.aspect, spp=args.spp)
+elif args.scene == "ch13":
+    cam = rtzig.chapter13_camera(width=args.width, spp=args.spp)
+else:
+    cam = rtzig.chapter9_camera(width=args.width, spp=args.spp)
 H, W = cam.height, cam.width
 NR = (H + args.row_step - 1) // args.row_step
 out = torch.empty((NR, W, 3), dtype=torch.float64, device="cuda:0")
@@ -70,4 +76,4 @@ for rnd in range(args.rounds + 1):
             times[path].append(a.value)
 res = {p: {"median_ms": round(statistics.median(t), 3), "min_ms": round(min(t), 3),
            "Msamples_s": round(W * NR * args.spp / statistics.median(t) / 1e3, 1)} for p, t in times.items()}
-print(json.dumps({"config": f"{W}x{H} {args.spp}spp rows 0::{args.row_step}", "results": res}))
+print(json.dumps({"config": f"{args.scene} {W}x{H} {args.spp}spp rows 0::{args.row_step}", "results": res}))

@@ -10,3 +10,5 @@ timeout -k 10 300 python -u bench.py > gpurun_out/bench.json 2> gpurun_out/bench
 rc=$?; echo "bench rc=$rc"; cat gpurun_out/bench.json; [ $rc -eq 0 ] || { tail -5 gpurun_out/bench.err; exit $rc; }
 timeout -k 10 200 python -u tools/rank_sim.py --spp 500 --reps 3 > gpurun_out/rank_sim.json 2> gpurun_out/rank_sim.err
 rc=$?; echo "rank_sim rc=$rc"; cat gpurun_out/rank_sim.json; [ $rc -eq 0 ] || { tail -5 gpurun_out/rank_sim.err; exit $rc; }
+timeout -k 10 400 python -u tools/configs_bench.py --out gpurun_out/r01_configs.json > gpurun_out/configs.log 2>&1
+rc=$?; echo "configs rc=$rc"; tail -6 gpurun_out/configs.log; [ $rc -eq 0 ] || exit $rc
