@@ -7,7 +7,7 @@ timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout
 rc=$?; echo "pytest rc=$rc"; tail -3 gpurun_out/pytest_gpu.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python -u bench.py ${BENCH_ARGS:-} > gpurun_out/bench.json 2> gpurun_out/bench.err
 rc=$?; echo "bench rc=$rc"; cat gpurun_out/bench.json; [ $rc -eq 0 ] || { tail -5 gpurun_out/bench.err; exit $rc; }
-timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
-  --master-port 29517 bench.py --gpus 2 --steps 2 --warmup 1 --dist-backend gloo > gpurun_out/bench_gloo2.json 2> gpurun_out/bench_gloo2.err
+timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node ${NPROC:-2} --master-addr 127.0.0.1 \
+  --master-port 29517 bench.py --gpus ${NPROC:-2} --steps 2 --warmup 1 --dist-backend gloo > gpurun_out/bench_gloo2.json 2> gpurun_out/bench_gloo2.err
 rc=$?; echo "gloo2 rc=$rc"; cat gpurun_out/bench_gloo2.json; [ $rc -eq 0 ] || tail -5 gpurun_out/bench_gloo2.err
 exit $rc
