@@ -270,14 +270,14 @@ __device__ __forceinline__ uint64_t sample_key(uint64_t seed_mix, uint64_t pixel
 }
 
 // Work-queue claim size (guided self-scheduling): a wave claims kChunk items while plenty remain
-// and ever smaller chunks as the queue drains, so waves run out of work within a few path lengths
-// of each other.  `seen` = an estimate of the queue position, `nwaves` = waves in the grid.  A
-// claim takes 1/K of an even share of what is left, (remaining / nwaves) / K, with K = 8 and a
-// floor of 256 items (4 per lane).  A/B (tools/gpu_abchunk.sh, profiles/r01_chunk): K = 2 -> 8
-// cut the kernel 6% on rank 0's rows of an 8-GPU job (8.35 -> 7.84 ms), 1% on the whole final
-// frame and on chapter 13; K = 12..32 are slower.  The floor matters on short frames: 128 items
-// cost chapter 9 (9 M items) 45% (more claims, each a wave-wide atomic round trip), 256..512 are
-// within noise of each other.
+// and ever smaller chunks as its queue segment drains, so waves run out of work within a few path
+// lengths of each other.  `seen` = an estimate of the segment's position, `nwaves` = waves
+// claiming from it.  A claim takes 1/K of an even share of what is left, (remaining / nwaves) / K,
+// with K = 8 and a floor of 64 items (1 per lane).  A/B (tools/gpu_abchunk.sh,
+// profiles/r01_chunk): K = 2 -> 8 cut the kernel 6% on rank 0's rows of an 8-GPU job and 1% on the
+// whole final frame and on chapter 13; K >= 12 is slower.  With ONE queue counter a floor below
+// 256 cost the short chapter 9 frame up to 45% (each claim is an atomic on that one address);
+// with 8 counters (rtk::kQueues) the 64-item floor is the fastest on every config.
 #ifndef RTZIG_GUIDED
 #define RTZIG_GUIDED 1
 #endif
@@ -285,7 +285,7 @@ __device__ __forceinline__ uint64_t sample_key(uint64_t seed_mix, uint64_t pixel
 #define RTZIG_GUIDED_K 8
 #endif
 #ifndef RTZIG_MIN_CHUNK
-#define RTZIG_MIN_CHUNK 256
+#define RTZIG_MIN_CHUNK 64
 #endif
 __device__ __forceinline__ uint64_t guided_chunk(uint64_t total, uint64_t seen, uint64_t nwaves, uint64_t max_chunk) {
 #if RTZIG_GUIDED

@@ -14,6 +14,19 @@ constexpr uint32_t kMaxLdsSpheres = 2048;  // 64 KiB of LDS geometry; above this
 #define RTZIG_CHUNK 2048
 #endif
 constexpr uint32_t kChunk = RTZIG_CHUNK;          // work items a wave claims per queue fetch (at most: guided_chunk)
+#ifndef RTZIG_QUEUES
+#define RTZIG_QUEUES 8
+#endif
+// Work-queue counters: the items of a launch are split into kQueues contiguous segments, one
+// counter each (kQueueStride u64 apart, separate 256-B lines); a wave claims from the segment of
+// its block (blockIdx % kQueues) and moves on to the next segments once that one is exhausted.
+// One counter serves ~88 claims per µs; 8 of them let the claims shrink to 64 items at the end of a
+// launch (A/B, profiles/r01_chunk: chapter 9 -8%, rank 0's N = 8 rows -1%, final frame -0.5%).
+constexpr uint32_t kQueues = RTZIG_QUEUES;
+constexpr uint32_t kQueueStride = 32;
+constexpr size_t kQueueBytes = (size_t)kQueues * kQueueStride * sizeof(unsigned long long);
+constexpr size_t kQueueBufferBytes = 4096;  // allocated by rt_runtime.cpp
+static_assert(kQueues >= 1 && kQueueBytes <= kQueueBufferBytes, "queue counters exceed the queue buffer");
 constexpr uint32_t kPad = 4;               // sphere list padded to a multiple of this (sentinels)
 #ifndef RTZIG_RUV_TRIPS
 #define RTZIG_RUV_TRIPS 3

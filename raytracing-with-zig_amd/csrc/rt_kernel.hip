@@ -8,7 +8,7 @@
 // Two kernels (DESIGN.md "Kernels"):
 //
 // sample_kernel — persistent waves pull work items (one item = one sample of one pixel) from a
-//   global queue, 2048 items per wave per atomic.  A lane whose path ends (miss / absorb /
+//   global queue (8 segments with a counter each, up to 2048 items per wave per atomic).  A lane whose path ends (miss / absorb /
 //   bounceMax) stores the sample's color and immediately takes the next item, so every lane of
 //   every wave traces one ray segment per loop iteration until the queue drains: no lane idles
 //   behind a long glass path and no CU idles behind a slow block.
@@ -626,6 +626,10 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
     // wave-uniform queue window [cur, end)
     uint64_t cur = 0, end = 0, last_chunk = 0;
     bool drained = false;
+    // claim segment (kQueues > 1): the block's own first, then the following ones
+    uint32_t qcur = kQueues == 1 ? 0 : blockIdx.x % kQueues, qmoves = 0;
+    uint64_t qend = 0;  // end of this wave's last claim, relative to its segment
+    const uint64_t qwaves = nwaves / kQueues > 0 ? nwaves / kQueues : 1;
 
     // per-lane path state
     bool active = false;
@@ -653,20 +657,37 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
         uint64_t needy = __ballot(!active);
         while (needy != 0 && !drained) {
             if (cur >= end) {
-                // guided claim, sized from an estimate of the queue position: this wave's previous
-                // claim plus one such claim by every other wave since (rtk::guided_chunk)
-                const uint64_t chunk = rtk::guided_chunk(total, end + nwaves * last_chunk, nwaves, kChunk);
-                last_chunk = chunk;
-                unsigned long long base = 0;
-                if (lane == 0) base = atomicAdd(queue, (unsigned long long)chunk);
-                base = __shfl(base, 0, 64);
-                if (base >= total) {
+                // guided claim from segment qcur, sized from an estimate of the segment's position:
+                // this wave's previous claim plus one such claim by every other wave of the segment
+                // since (rtk::guided_chunk); an exhausted segment sends the wave on to the next one
+                // (at most kQueues - 1 moves per wave, so every wave reaches `drained`)
+                bool got = false;
+                while (!got && qmoves < kQueues) {
+                    const uint32_t q = qcur;
+                    const uint64_t s0 = kQueues == 1 ? 0 : total * q / kQueues;
+                    const uint64_t s1 = kQueues == 1 ? total : total * (q + 1) / kQueues;
+                    const uint64_t chunk = qmoves == 0
+                        ? rtk::guided_chunk(s1 - s0, qend + qwaves * last_chunk, qwaves, kChunk)
+                        : (uint64_t)RTZIG_MIN_CHUNK;  // another segment's tail: smallest claims
+                    last_chunk = chunk;
+                    unsigned long long base = 0;
+                    if (lane == 0) base = atomicAdd(queue + (size_t)q * kQueueStride, (unsigned long long)chunk);
+                    base = __shfl(base, 0, 64);
+                    if (base < s1 - s0) {
+                        cur = s0 + base;
+                        qend = base + chunk < s1 - s0 ? base + chunk : s1 - s0;
+                        end = s0 + qend;
+                        got = true;
+                    } else {
+                        ++qmoves;
+                        qcur = qcur + 1 == kQueues ? 0 : qcur + 1;
+                    }
+                }
+                if (!got) {
                     drained = true;
                     if constexpr (kProf) rt_drain = __builtin_amdgcn_s_memrealtime();
                     break;
                 }
-                cur = base;
-                end = base + chunk < total ? base + chunk : total;
             }
             const uint64_t avail = end - cur;
             const uint32_t want = (uint32_t)__popcll(needy);
@@ -1122,7 +1143,7 @@ extern "C" hipError_t rtk_launch_samples(const rtk::KernelParams* p, const rtk::
     const uint64_t need = (total + kBlock - 1) / kBlock;
     auto* st = (unsigned long long*)stats;
     auto* qu = (unsigned long long*)queue;
-    hipError_t e = hipMemsetAsync(queue, 0, sizeof(unsigned long long), stream);
+    hipError_t e = hipMemsetAsync(queue, 0, kQueueBytes, stream);
     if (e != hipSuccess) return e;
     if (name) *name = v.name;
 #define RTK_CASE(L, U, W)                                                                 \
@@ -1149,7 +1170,7 @@ extern "C" hipError_t rtk_launch_samples_bvh(const rtk::KernelParams* p, const r
     const bool lds_scene = stack_bytes + scene_bytes <= 80 * 1024;
     const size_t shmem = stack_bytes + (lds_scene ? scene_bytes : 0);
     const uint64_t need = (total + kBlockBvh - 1) / kBlockBvh;
-    hipError_t e = hipMemsetAsync(queue, 0, sizeof(unsigned long long), stream);
+    hipError_t e = hipMemsetAsync(queue, 0, kQueueBytes, stream);
     if (e != hipSuccess) return e;
     auto* st = (unsigned long long*)stats;
     auto* qu = (unsigned long long*)queue;
