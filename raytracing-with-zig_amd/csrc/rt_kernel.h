@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "rt_device.h"
 #include "rt_fastdiv.h"
 
 namespace rtk {
@@ -27,6 +28,43 @@ constexpr uint32_t kQueueStride = 32;
 constexpr size_t kQueueBytes = (size_t)kQueues * kQueueStride * sizeof(unsigned long long);
 constexpr size_t kQueueBufferBytes = 4096;  // allocated by rt_runtime.cpp
 static_assert(kQueues >= 1 && kQueueBytes <= kQueueBufferBytes, "queue counters exceed the queue buffer");
+// Wave-uniform claim state of the segmented work queue (path_loop, path_loop_fast).  claim()
+// fetches a new window [cur, end) of item numbers: a guided claim from the wave's current segment,
+// sized from an estimate of that segment's position (this wave's previous claim plus one such claim
+// by every other wave of the segment since, rtk::guided_chunk); an exhausted segment sends the wave
+// on to the next one, where it claims RTZIG_MIN_CHUNK items at a time.  After kQueues failed claims
+// (one per segment) it returns false for good, so every wave reaches the drained state.
+struct WorkQueue {
+    uint64_t total, seg_waves;
+    uint64_t cur = 0, end = 0, qend = 0, last_chunk = 0;
+    uint32_t qcur, qmoves = 0;
+    __device__ WorkQueue(uint64_t total_, uint64_t nwaves, uint32_t block)
+        : total(total_), seg_waves(nwaves / kQueues > 0 ? nwaves / kQueues : 1),
+          qcur(kQueues == 1 ? 0 : block % kQueues) {}
+    __device__ __forceinline__ bool claim(unsigned long long* __restrict__ queue, uint32_t lane) {
+        while (qmoves < kQueues) {
+            const uint32_t q = qcur;
+            const uint64_t s0 = kQueues == 1 ? 0 : total * q / kQueues;
+            const uint64_t s1 = kQueues == 1 ? total : total * (q + 1) / kQueues;
+            const uint64_t chunk = qmoves == 0 ? guided_chunk(s1 - s0, qend + seg_waves * last_chunk, seg_waves, kChunk)
+                                               : (uint64_t)RTZIG_MIN_CHUNK;
+            last_chunk = chunk;
+            unsigned long long base = 0;
+            if (lane == 0) base = atomicAdd(queue + (size_t)q * kQueueStride, (unsigned long long)chunk);
+            base = __shfl(base, 0, 64);
+            if (base < s1 - s0) {
+                qend = base + chunk < s1 - s0 ? base + chunk : s1 - s0;
+                cur = s0 + base;
+                end = s0 + qend;
+                return true;
+            }
+            ++qmoves;
+            qcur = qcur + 1 == kQueues ? 0 : qcur + 1;
+        }
+        return false;
+    }
+};
+
 constexpr uint32_t kPad = 4;               // sphere list padded to a multiple of this (sentinels)
 #ifndef RTZIG_RUV_TRIPS
 #define RTZIG_RUV_TRIPS 3

@@ -623,13 +623,9 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
     const uint32_t lane = lane_id();
     const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x / 64);
 
-    // wave-uniform queue window [cur, end)
-    uint64_t cur = 0, end = 0, last_chunk = 0;
+    // wave-uniform queue window [wq.cur, wq.end) and claim state
+    WorkQueue wq(total, nwaves, blockIdx.x);
     bool drained = false;
-    // claim segment (kQueues > 1): the block's own first, then the following ones
-    uint32_t qcur = kQueues == 1 ? 0 : blockIdx.x % kQueues, qmoves = 0;
-    uint64_t qend = 0;  // end of this wave's last claim, relative to its segment
-    const uint64_t qwaves = nwaves / kQueues > 0 ? nwaves / kQueues : 1;
 
     // per-lane path state
     bool active = false;
@@ -656,51 +652,25 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
         bool fresh = false;
         uint64_t needy = __ballot(!active);
         while (needy != 0 && !drained) {
-            if (cur >= end) {
-                // guided claim from segment qcur, sized from an estimate of the segment's position:
-                // this wave's previous claim plus one such claim by every other wave of the segment
-                // since (rtk::guided_chunk); an exhausted segment sends the wave on to the next one
-                // (at most kQueues - 1 moves per wave, so every wave reaches `drained`)
-                bool got = false;
-                while (!got && qmoves < kQueues) {
-                    const uint32_t q = qcur;
-                    const uint64_t s0 = kQueues == 1 ? 0 : total * q / kQueues;
-                    const uint64_t s1 = kQueues == 1 ? total : total * (q + 1) / kQueues;
-                    const uint64_t chunk = qmoves == 0
-                        ? rtk::guided_chunk(s1 - s0, qend + qwaves * last_chunk, qwaves, kChunk)
-                        : (uint64_t)RTZIG_MIN_CHUNK;  // another segment's tail: smallest claims
-                    last_chunk = chunk;
-                    unsigned long long base = 0;
-                    if (lane == 0) base = atomicAdd(queue + (size_t)q * kQueueStride, (unsigned long long)chunk);
-                    base = __shfl(base, 0, 64);
-                    if (base < s1 - s0) {
-                        cur = s0 + base;
-                        qend = base + chunk < s1 - s0 ? base + chunk : s1 - s0;
-                        end = s0 + qend;
-                        got = true;
-                    } else {
-                        ++qmoves;
-                        qcur = qcur + 1 == kQueues ? 0 : qcur + 1;
-                    }
-                }
-                if (!got) {
+            if (wq.cur >= wq.end) {
+                if (!wq.claim(queue, lane)) {
                     drained = true;
                     if constexpr (kProf) rt_drain = __builtin_amdgcn_s_memrealtime();
                     break;
                 }
             }
-            const uint64_t avail = end - cur;
+            const uint64_t avail = wq.end - wq.cur;
             const uint32_t want = (uint32_t)__popcll(needy);
             const uint32_t take = avail < want ? (uint32_t)avail : want;
             if (!active) {
                 const uint32_t rk = rank_in(needy);
                 if (rk < take) {
-                    item = cur + rk;
+                    item = wq.cur + rk;
                     active = true;
                     fresh = true;
                 }
             }
-            cur += take;
+            wq.cur += take;
             needy = __ballot(!active);
         }
         // the lanes handed an item above start their path: seeding and getRay run once, outside

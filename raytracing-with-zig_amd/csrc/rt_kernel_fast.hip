@@ -34,6 +34,7 @@ using rtk::GeoRec;
 using rtk::KernelParams;
 using rtk::kBlockBvh;
 using rtk::kChunk;
+using rtk::WorkQueue;
 using rtk::kLeafBvh;
 using rtk::MatRec;
 using rtk::Rng;
@@ -314,7 +315,7 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
     const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x / 64);
     const float t_min = (float)p.t_min, t_max = (float)p.t_max;
 
-    uint64_t cur = 0, end = 0, last_chunk = 0;
+    WorkQueue wq(total, nwaves, blockIdx.x);  // segmented queue (rt_kernel.h), as the parity kernel
     bool drained = false;
     bool active = false, pending = false, sc_metal = false, dpend = false;
     uint64_t item = 0, slot = 0;
@@ -330,33 +331,22 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
         bool fresh = false;
         uint64_t needy = __ballot(!active);
         while (needy != 0 && !drained) {
-            if (cur >= end) {
-                // guided claim, sized from an estimate of the queue position: this wave's previous
-                // claim plus one such claim by every other wave since (rtk::guided_chunk)
-                const uint64_t chunk = rtk::guided_chunk(total, end + nwaves * last_chunk, nwaves, kChunk);
-                last_chunk = chunk;
-                unsigned long long base = 0;
-                if (lane == 0) base = atomicAdd(queue, (unsigned long long)chunk);
-                base = __shfl(base, 0, 64);
-                if (base >= total) {
-                    drained = true;
-                    break;
-                }
-                cur = base;
-                end = base + chunk < total ? base + chunk : total;
+            if (wq.cur >= wq.end && !wq.claim(queue, lane)) {
+                drained = true;
+                break;
             }
-            const uint64_t avail = end - cur;
+            const uint64_t avail = wq.end - wq.cur;
             const uint32_t want = (uint32_t)__popcll(needy);
             const uint32_t take = avail < want ? (uint32_t)avail : want;
             if (!active) {
                 const uint32_t rk = rank_in(needy);
                 if (rk < take) {
-                    item = cur + rk;
+                    item = wq.cur + rk;
                     active = true;
                     fresh = true;
                 }
             }
-            cur += take;
+            wq.cur += take;
             needy = __ballot(!active);
         }
         // the lanes handed an item above start their path: seeding and getRay run once, outside
@@ -540,7 +530,7 @@ extern "C" hipError_t rtk_launch_samples_fast(const rtk::KernelParams* p, const 
     const bool lds_scene = stack_bytes + scene_bytes <= 80 * 1024;
     const size_t shmem = stack_bytes + (lds_scene ? scene_bytes : 0);
     const uint64_t need = (total + kBlockBvh - 1) / kBlockBvh;
-    hipError_t e = hipMemsetAsync(queue, 0, sizeof(unsigned long long), stream);
+    hipError_t e = hipMemsetAsync(queue, 0, kQueueBytes, stream);
     if (e != hipSuccess) return e;
     auto launch = [&](auto kernel, const char* nm) -> hipError_t {
         uint32_t cap32 = 0;

@@ -404,7 +404,7 @@ int rt_render_rows_async(rt_context* ctx, const rt_camera* cam, uint32_t output_
     if (!rc && n_chunks > 1) rc = ensure_buffer((void**)&ctx->d_sums, &ctx->sums_bytes, layer);
     if (!rc && !ctx->d_queue) {
         size_t qb = 0;
-        rc = ensure_buffer((void**)&ctx->d_queue, &qb, 4096);  // rtk::kQueueBufferBytes: up to 16 queue counters
+        rc = ensure_buffer((void**)&ctx->d_queue, &qb, rtk::kQueueBufferBytes);
     }
     if (rc) return rc;
 
