@@ -60,10 +60,20 @@ def cpu_baseline(width, aspect, cpu_spp):
     _, rays = o.render_a(cam, spheres, state)
     dt = time.perf_counter() - t0
     n = cam.image_width * cam.image_height * cpu_spp
-    return {"value": round(n / dt / 1e6, 4), "unit": "Msamples/s", "cores": 1, "kind": "port",
-            "sample": f"oracle A (C restatement of the Zig reference, sequential RNG stream, -O3) "
-                      f"full {cam.image_width}x{cam.image_height} frame at {cpu_spp} spp "
-                      f"({n} samples, {rays} rays) in {dt:.2f} s"}
+    res = {"value": round(n / dt / 1e6, 4), "unit": "Msamples/s", "cores": 1, "kind": "port",
+           "sample": f"oracle A (C restatement of the Zig reference, sequential RNG stream, -O3) "
+                     f"full {cam.image_width}x{cam.image_height} frame at {cpu_spp} spp "
+                     f"({n} samples, {rays} rays) in {dt:.2f} s"}
+    # context only: oracle B, the same arithmetic with per-(pixel, sample) streams,
+    # parallel over rows with OpenMP on this job's share of the host cores (at most 16)
+    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    t0 = time.perf_counter()
+    o.render_b(cam, spheres, threads=threads)
+    dtb = time.perf_counter() - t0
+    res["multicore_context"] = {"value": round(n / dtb / 1e6, 4), "unit": "Msamples/s", "cores": threads,
+                                "kind": "port (oracle B, OpenMP over rows)",
+                                "sample": f"same frame, {dtb:.2f} s"}
+    return res
 
 
 def pmc_traffic(workload):
