@@ -111,7 +111,7 @@ struct KernelParams {
     uint32_t n_pad;  // n_spheres rounded up to kPad (sentinel-padded)
     uint32_t s_begin, s_count;
     uint32_t prof;   // 1: instrumented build, stats has 8 entries (see rt_context_enable_profile)
-    uint32_t order;  // work-item order: 0 sample-major, 1 pixel-major (RTZIG_ORDER)
+    uint32_t order;  // work-item order: 0 sample-major, 1 pixel-major, 2 sample-major over 8x8 tiles (RTZIG_ORDER)
     uint32_t pad2;
     FastDiv div_layer;  // / (n_rows * width): item -> (sample, pixel) in the refill
     FastDiv div_width;  // / width: pixel -> (row, column)

@@ -679,16 +679,41 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
             // items per launch < 2^32 (host-side chunking): 32-bit index math
             const uint32_t it32 = (uint32_t)item;
             uint32_t s_local, q;
-            if (p.order == 0) {  // sample-major: a wave takes 64 neighbouring pixels
+            uint32_t row_local, i;
+            if (p.order == 0) {  // sample-major: a wave takes 64 neighbouring pixels of one row
                 s_local = fastdiv(it32, p.div_layer);
                 q = it32 - s_local * P;
+                row_local = fastdiv(q, p.div_width);
+                i = q - row_local * W;
+            } else if (p.order == 2) {
+                // sample-major over 8x8 pixel tiles: bands of 8 rows, each walked tile by tile (8
+                // columns x the band's rows, row-major inside a tile); q is the position in that order
+                s_local = fastdiv(it32, p.div_layer);
+                q = it32 - s_local * P;
+                const uint32_t band = fastdiv(q, p.div_width) >> 3;
+                const uint32_t rq = q - band * 8 * W;
+                const uint32_t hb = p.n_rows - band * 8 < 8 ? p.n_rows - band * 8 : 8;
+                uint32_t c, o, orow, wc;
+                if (hb == 8 && (rq >> 6) * 8 + 8 <= W) {  // a full tile: shifts
+                    c = rq >> 6;
+                    o = rq & 63;
+                    orow = o >> 3;
+                    wc = 8;
+                } else {  // the last band (n_rows % 8) or the last tile column (W % 8)
+                    c = rq / (8 * hb);
+                    o = rq - c * 8 * hb;
+                    wc = W - c * 8 < 8 ? W - c * 8 : 8;
+                    orow = o / wc;
+                }
+                i = c * 8 + (o - orow * wc);
+                row_local = band * 8 + orow;
             } else {  // pixel-major: a wave takes consecutive samples of one pixel
                 q = it32 / p.s_count;
                 s_local = it32 - q * p.s_count;
+                row_local = fastdiv(q, p.div_width);
+                i = q - row_local * W;
             }
-            slot = (uint64_t)s_local * P + q;
-            const uint32_t row_local = fastdiv(q, p.div_width);
-            const uint32_t i = q - row_local * W;
+            slot = (uint64_t)s_local * P + (row_local * W + i);
             const uint32_t j = p.row0 + row_local * p.row_step;
             const uint64_t pixel = (uint64_t)j * W + i;
             g.seed(sample_key(p.seed_mix, pixel, p.s_begin + s_local));

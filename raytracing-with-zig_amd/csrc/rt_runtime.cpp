@@ -431,7 +431,8 @@ int rt_render_rows_async(rt_context* ctx, const rt_camera* cam, uint32_t output_
     const bool bvh = use_bvh(ctx);
     rtk::KernelParams p = make_params(cam, output_format, row0, row_step, n_rows, ctx->n_spheres);
     p.prof = ctx->profile && d_stats ? 1u : 0u;
-    if (const char* e = std::getenv("RTZIG_ORDER")) p.order = std::strcmp(e, "pixel") == 0 ? 1u : 0u;
+    if (const char* e = std::getenv("RTZIG_ORDER"))
+        p.order = std::strcmp(e, "pixel") == 0 ? 1u : (std::strcmp(e, "tile") == 0 ? 2u : 0u);
     for (uint32_t c = 0; c < n_chunks; c++) {
         p.s_begin = (uint32_t)(c * s_chunk);
         p.s_count = (uint32_t)std::min<uint64_t>(s_chunk, cam->samples_per_pixel - p.s_begin);

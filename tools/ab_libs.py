@@ -41,7 +41,10 @@ H, W = cam.height, cam.width
 NR = (H + args.row_step - 1) // args.row_step
 out = torch.empty((NR, W, 3), dtype=torch.float64, device="cuda:0")
 runs = []
-for path in args.libs:
+envs = {}
+for spec in args.libs:  # "lib.so" or "lib.so:VAR=VAL" (an environment variable set around its renders)
+    path, _, env = spec.partition(":")
+    envs[spec] = tuple(env.split("=", 1)) if env else None
     L = C.CDLL(os.path.abspath(path))
     vp = C.c_void_p
     for name, res, argt in [("rt_context_create", C.c_int, [C.c_int, C.POINTER(vp)]),
@@ -57,14 +60,18 @@ for path in args.libs:
     assert L.rt_context_create(0, C.byref(ctx)) == 0, L.rt_last_error()
     assert L.rt_context_set_scene(ctx, cam.scene.world, len(cam.scene.world)) == 0, L.rt_last_error()
     assert L.rt_context_enable_timing(ctx, 1) == 0
-    runs.append((path, L, ctx))
+    runs.append((spec, L, ctx))
 times = {p: [] for p, _, _ in runs}
 ref = None
 for rnd in range(args.rounds + 1):
     for path, L, ctx in runs:
+        if envs[path]:
+            os.environ[envs[path][0]] = envs[path][1]
         rc = L.rt_render_rows_async(ctx, C.byref(cam.cam), 0, 0, args.row_step, NR, C.c_void_p(out.data_ptr()), None, None)
         assert rc == 0, L.rt_last_error()
         torch.cuda.synchronize()
+        if envs[path]:
+            del os.environ[envs[path][0]]
         a, b = C.c_double(), C.c_double()
         assert L.rt_context_kernel_times(ctx, C.byref(a), C.byref(b)) == 0
         img = out.cpu()
