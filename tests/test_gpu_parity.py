@@ -230,6 +230,31 @@ def test_walk_variants_bit_exact(oracle, variant, monkeypatch):
     assert np.array_equal(out, ref)
 
 
+@pytest.mark.parametrize("order", ["pixel", "tile"])
+def test_work_orders_bit_exact(oracle, order, monkeypatch):
+    """The optional work-item orders (RTZIG_ORDER: pixel-major, 8x8 tiles) hand out every (pixel,
+    sample) exactly once and give oracle B's bits, including partial tiles (W, rows not multiples
+    of 8) and interleaved row sets."""
+    import torch
+    monkeypatch.setenv("RTZIG_ORDER", order)
+    cam = rtzig.final_scene_camera(width=203, aspect_ratio=16 / 9, spp=5)
+    out, st = gpu_render(cam, cam.scene.world, n_gpus=1)
+    ref, rays = oracle.render_b(cam.cam, cam.scene.world, threads=8)
+    assert np.array_equal(out, ref) and st["rays"] == rays
+    H = cam.height
+    for row0, step in [(0, 8), (3, 8), (1, 3)]:
+        n = (H - row0 + step - 1) // step
+        part, _ = oracle.render_b(cam.cam, cam.scene.world, row0=row0, row_step=step, n_rows=n, threads=8)
+        assert np.array_equal(part, ref[row0::step])
+        r = rtzig.DeviceRenderer(0)
+        r.set_scene(cam.scene.world)
+        d = torch.empty((n, cam.width, 3), dtype=torch.float64, device="cuda:0")
+        r.render_rows_async(cam.cam, d.data_ptr(), row0=row0, row_step=step, n_rows=n)
+        torch.cuda.synchronize()
+        assert np.array_equal(d.cpu().numpy(), part)
+        r.close()
+
+
 @pytest.mark.parametrize("always_area", [None, "0", "1e-6"])
 @pytest.mark.parametrize("seed", [1, 2, 3])
 def test_bvh_random_scenes_bit_exact(oracle, seed, always_area, monkeypatch):
