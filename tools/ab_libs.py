@@ -58,7 +58,11 @@ for spec in args.libs:  # "lib.so" or "lib.so:VAR=VAL" (an environment variable 
         getattr(L, name).argtypes = argt
     ctx = C.c_void_p()
     assert L.rt_context_create(0, C.byref(ctx)) == 0, L.rt_last_error()
+    if envs[spec]:  # build-time knobs (the BVH is built in set_scene) as well as render-time ones
+        os.environ[envs[spec][0]] = envs[spec][1]
     assert L.rt_context_set_scene(ctx, cam.scene.world, len(cam.scene.world)) == 0, L.rt_last_error()
+    if envs[spec]:
+        del os.environ[envs[spec][0]]
     assert L.rt_context_enable_timing(ctx, 1) == 0
     runs.append((spec, L, ctx))
 times = {p: [] for p, _, _ in runs}
