@@ -998,6 +998,9 @@ __global__ __launch_bounds__(kBlockBvh) void sample_kernel_bvh(KernelParams p, B
                      mat_g, samples, queue, stats);
 }
 
+#ifndef RTZIG_REDUCE_NT
+#define RTZIG_REDUCE_NT 0
+#endif
 template <int kOut>
 __global__ __launch_bounds__(256) void reduce_kernel(ReduceParams p, const double* __restrict__ samples,
                                                      double* __restrict__ sums, void* __restrict__ out) {
@@ -1013,9 +1016,16 @@ __global__ __launch_bounds__(256) void reduce_kernel(ReduceParams p, const doubl
     const uint64_t stride = 3 * (uint64_t)p.n_pixels;
 #pragma unroll 8
     for (uint32_t s = 0; s < p.s_count; ++s) {
+#if RTZIG_REDUCE_NT
+        // streamed once: non-temporal loads (no reuse to keep in L2 / MALL)
+        x = x + __builtin_nontemporal_load(src + 0);
+        y = y + __builtin_nontemporal_load(src + 1);
+        z = z + __builtin_nontemporal_load(src + 2);
+#else
         x = x + src[0];
         y = y + src[1];
         z = z + src[2];
+#endif
         src += stride;
     }
     if (!p.last) {

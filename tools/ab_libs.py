@@ -66,6 +66,7 @@ for spec in args.libs:  # "lib.so" or "lib.so:VAR=VAL" (an environment variable 
     assert L.rt_context_enable_timing(ctx, 1) == 0
     runs.append((spec, L, ctx))
 times = {p: [] for p, _, _ in runs}
+rtimes = {p: [] for p, _, _ in runs}
 ref = None
 for rnd in range(args.rounds + 1):
     for path, L, ctx in runs:
@@ -85,6 +86,8 @@ for rnd in range(args.rounds + 1):
             assert torch.equal(img, ref), f"{path} output differs"
         if rnd > 0:
             times[path].append(a.value)
+            rtimes[path].append(b.value)
 res = {p: {"median_ms": round(statistics.median(t), 3), "min_ms": round(min(t), 3),
-           "Msamples_s": round(W * NR * args.spp / statistics.median(t) / 1e3, 1)} for p, t in times.items()}
+           "Msamples_s": round(W * NR * args.spp / statistics.median(t) / 1e3, 1),
+           "reduce_median_ms": round(statistics.median(rtimes[p]), 4)} for p, t in times.items()}
 print(json.dumps({"config": f"{args.scene} {W}x{H} {args.spp}spp rows 0::{args.row_step}", "results": res}))
