@@ -998,12 +998,63 @@ __global__ __launch_bounds__(kBlockBvh) void sample_kernel_bvh(KernelParams p, B
                      mat_g, samples, queue, stats);
 }
 
+#ifndef RTZIG_REDUCE_COAL
+#define RTZIG_REDUCE_COAL 0
+#endif
 #ifndef RTZIG_REDUCE_NT
 #define RTZIG_REDUCE_NT 0
 #endif
 template <int kOut>
 __global__ __launch_bounds__(256) void reduce_kernel(ReduceParams p, const double* __restrict__ samples,
                                                      double* __restrict__ sums, void* __restrict__ out) {
+#if RTZIG_REDUCE_COAL
+    // element-wise: thread t of block b sums the elements e = 768 b + t + 256 k (k = 0..2) of every
+    // [pixel][channel] sample layer.  Each channel's sum is independent and runs in sample order,
+    // so the additions are those of the per-pixel form; every load and store of a wave is one
+    // contiguous 512-B run instead of three 24-B-strided ones.
+    {
+        const uint64_t n_el = 3 * (uint64_t)p.n_pixels;
+        const uint64_t e0 = 768 * (uint64_t)blockIdx.x + threadIdx.x;
+        const bool v0 = e0 < n_el, v1 = e0 + 256 < n_el, v2 = e0 + 512 < n_el;
+        double a0 = 0.0, a1 = 0.0, a2 = 0.0;
+        if (!p.first) {
+            if (v0) a0 = sums[e0];
+            if (v1) a1 = sums[e0 + 256];
+            if (v2) a2 = sums[e0 + 512];
+        }
+        const double* src = samples + e0;
+        if (v2) {
+#pragma unroll 8
+            for (uint32_t s = 0; s < p.s_count; ++s) {
+                a0 = a0 + src[0];
+                a1 = a1 + src[256];
+                a2 = a2 + src[512];
+                src += n_el;
+            }
+        } else {  // the last block
+            for (uint32_t s = 0; s < p.s_count; ++s) {
+                if (v0) a0 = a0 + src[0];
+                if (v1) a1 = a1 + src[256];
+                src += n_el;
+            }
+        }
+        const double a[3] = {a0, a1, a2};
+        const bool v[3] = {v0, v1, v2};
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            if (!v[k]) continue;
+            const uint64_t e = e0 + 256 * k;
+            if (!p.last) {
+                sums[e] = a[k];
+            } else if constexpr (kOut == 0) {
+                ((double*)out)[e] = a[k] * p.scale;  // avgColor = pixelColor * pixelSamplesScale
+            } else {
+                ((uint8_t*)out)[e] = to_byte(a[k] * p.scale);
+            }
+        }
+        return;
+    }
+#endif
     const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
     if (q >= p.n_pixels) return;
     double x = 0.0, y = 0.0, z = 0.0;
