@@ -8,8 +8,9 @@
 // Two kernels (DESIGN.md "Kernels"):
 //
 // sample_kernel — persistent waves pull work items (one item = one sample of one pixel) from a
-//   global queue (8 segments with a counter each, up to 2048 items per wave per atomic).  A lane whose path ends (miss / absorb /
-//   bounceMax) stores the sample's color and immediately takes the next item, so every lane of
+//   global queue (8 segments with a counter each, up to 2048 items per wave per atomic).  A lane
+//   whose path ends (miss / absorb / bounceMax) stores the sample's color and immediately takes
+//   the next item, so every lane of
 //   every wave traces one ray segment per loop iteration until the queue drains: no lane idles
 //   behind a long glass path and no CU idles behind a slow block.
 //   Sphere geometry {cx, cy, cz, r^2} is staged once per workgroup into LDS (32 B per sphere);
