@@ -3,7 +3,7 @@
 # on chapter 9, chapter 13, the final scene, and rank 0's row set of an 8-GPU job.
 cd "$GRAFT_REPO_ROOT" || exit 2
 mkdir -p gpurun_out
-L=${AB:-"ab/c256.so ab/c128k8.so"}
+L=${AB:-"ab/base.so ab/new.so"}
 run() {  # name, args...
   local n=$1; shift
   timeout -k 10 200 python -u tools/ab_libs.py $L "$@" > gpurun_out/ab_$n.json 2> gpurun_out/ab_$n.err
