@@ -15,6 +15,9 @@ constexpr uint32_t kMaxLdsSpheres = 2048;  // 64 KiB of LDS geometry; above this
 #define RTZIG_CHUNK 2048
 #endif
 constexpr uint32_t kChunk = RTZIG_CHUNK;          // work items a wave claims per queue fetch (at most: guided_chunk)
+#ifndef RTZIG_QUEUE_HOME
+#define RTZIG_QUEUE_HOME 0  // 1: segment (block / kQueues) % kQueues (A/B knob)
+#endif
 #ifndef RTZIG_QUEUES
 #define RTZIG_QUEUES 8
 #endif
@@ -40,7 +43,7 @@ struct WorkQueue {
     uint32_t qcur, qmoves = 0;
     __device__ WorkQueue(uint64_t total_, uint64_t nwaves, uint32_t block)
         : total(total_), seg_waves(nwaves / kQueues > 0 ? nwaves / kQueues : 1),
-          qcur(kQueues == 1 ? 0 : block % kQueues) {}
+          qcur(kQueues == 1 ? 0 : (RTZIG_QUEUE_HOME ? block / kQueues : block) % kQueues) {}
     __device__ __forceinline__ bool claim(unsigned long long* __restrict__ queue, uint32_t lane) {
         while (qmoves < kQueues) {
             const uint32_t q = qcur;
