@@ -7,17 +7,24 @@ reference src/camera.zig:123-145) on the final random-sphere scene — BASELINE.
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 
-A step = one full frame: every rank renders its rows (HIP kernel via the C ABI, inputs resident in
-HBM) and the rows are gathered to rank 0 over RCCL.  The image is fixed, so N>1 is strong scaling.
-Rank 0 prints ONE JSON line.  `roofline` is the dominant kernel's FP64-VALU roofline (17 FLOPs per
-ray-sphere candidate test x spheres x rays); `cpu_baseline` times the oracle's
-sequential-stream port of the reference (single thread — the reference's single RNG stream is
-inherently sequential) on a bounded sample of the same frame.
+A step = one full frame: every rank renders its rows (one HIP kernel launch via the C ABI, inputs
+resident in HBM) and the rows are gathered to rank 0 over RCCL.  The image is fixed, so N>1 is
+strong scaling.  Rank 0 prints ONE JSON line.
+
+`roofline` is the dominant kernel's VALU roofline (bound "valu": no GEMM-shaped work on this path,
+DESIGN.md §5): achieved = the FLOPs the sample kernel executes per frame (exact in-kernel counts of
+one instrumented frame: 17 f64 FLOPs per ray-sphere candidate test, SURVEY §8(d)'s unit, plus 24 f32
+FLOPs per BVH node visit counted at half weight) / its HIP-event time, against the 78.6 TFLOP/s FP64
+vector peak.  `roofline.issue` is the VALU-issue cycle model from the committed PMC summary.
+`cpu_baseline` times the oracle's sequential-stream port of the reference (single thread — the
+reference's single RNG stream is inherently sequential) on a bounded sample of the same frame.
 """
 import argparse
 import json
 import os
+import subprocess
 import sys
+import tempfile
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -31,25 +38,37 @@ import rtzig  # noqa: E402
 from rtzig import dist as rdist  # noqa: E402
 
 METRIC = "Msamples/sec (pixels×spp/s) on final-render scene; achieved HBM GB/s vs peak"
-FP64_VALU_PEAK_TFLOPS = 78.6   # MI355X dense FP64 (spec), vector and matrix pipes alike
+FP64_VALU_PEAK_TFLOPS = 78.6   # MI355X vector FP64 (spec) = unpacked FP32 at half weight
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E (spec), MI355X_MICROARCH.md
+SIMDS = 1024                   # 256 CUs x 4 SIMDs
 FLOPS_PER_TEST = 17            # oc(3) + h(5) + |oc|^2(5) + -r^2(1) + h^2-a*c(3), SURVEY §8(d)
-F32_FLOPS_PER_VISIT = 24       # BVH node visit: 2 child boxes x 3 axes x 2 planes x (sub + mul), f32
+F32_FLOPS_PER_VISIT = 24       # BVH node visit: 2 child boxes x 3 axes x 2 planes x fma (2 FLOPs), f32
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+def _oracle():
+    """Oracle A's CPU baseline build: SURVEY §8(d)'s flags (-O3 -march=native -ffp-contract=off),
+    compiled here for this host's CPU; the portable build if that fails."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from oracle_lib import Oracle
+    d = tempfile.mkdtemp(prefix="rtzig_oracle_")
+    try:
+        subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "native", f"NATIVE_DIR={d}"],
+                       check=True, capture_output=True, timeout=120)
+        return Oracle(os.path.join(d, "liboracle.so")), "-O3 -march=native -ffp-contract=off (built on this host)"
+    except Exception as e:  # noqa: BLE001
+        log(f"native oracle build failed ({e}); using the portable build")
+        return Oracle(), "-O3 -ffp-contract=off (portable build)"
+
+
 def cpu_baseline(width, aspect, cpu_spp):
     """Oracle A (reference port, sequential Xoshiro stream, one thread) on a bounded sample:
     the full config-4 frame at `cpu_spp` samples per pixel."""
-    sys.path.insert(0, os.path.join(ROOT, "tests"))
-    import ctypes as C
-
-    from oracle_lib import Oracle
     from rtzig.abi import D3, RtCameraParams
-    o = Oracle()
+    o, flags = _oracle()
     spheres, state = o.scene_final(0xDEADBEEF)
     p = RtCameraParams(image_width=width, samples_per_pixel=cpu_spp, bounce_max=50,
                        aspect_ratio=aspect, look_from=D3(13, 2, 3), look_at=D3(0, 0, 0),
@@ -61,7 +80,7 @@ def cpu_baseline(width, aspect, cpu_spp):
     dt = time.perf_counter() - t0
     n = cam.image_width * cam.image_height * cpu_spp
     res = {"value": round(n / dt / 1e6, 4), "unit": "Msamples/s", "cores": 1, "kind": "port",
-           "sample": f"oracle A (C restatement of the Zig reference, sequential RNG stream, -O3) "
+           "sample": f"oracle A (C restatement of the Zig reference, sequential RNG stream, {flags}) "
                      f"full {cam.image_width}x{cam.image_height} frame at {cpu_spp} spp "
                      f"({n} samples, {rays} rays) in {dt:.2f} s"}
     # context only: oracle B, the same arithmetic with per-(pixel, sample) streams,
@@ -76,17 +95,26 @@ def cpu_baseline(width, aspect, cpu_spp):
     return res
 
 
-def pmc_traffic(workload):
-    """HBM bytes per launch from the committed rocprofv3 PMC summary (profiles/pmc_traffic.json,
-    written by tools/pmc_traffic.py from separate FETCH_SIZE / WRITE_SIZE passes), or None."""
-    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+def pmc_summary(workload):
+    """Per-frame PMC figures of the timed sample kernel from the committed rocprofv3 summary
+    (profiles/pmc_traffic.json, written by tools/pmc_summary.py from separate --pmc passes), or {}."""
     try:
-        d = json.load(open(path))
+        d = json.load(open(os.path.join(ROOT, "profiles", "pmc_traffic.json")))
     except (OSError, ValueError):
-        return None
-    if d.get("workload") != workload:
-        return None
-    return d.get("hbm_bytes_per_launch")
+        return {}
+    return d if d.get("workload") == workload else {}
+
+
+def dropin(cam, device):
+    """The drop-in path's end-to-end cost: rt_render (n_gpus=1) of the same frame into host memory,
+    cold (first call of the process: context, scene + BVH upload, workspace, render, D2H) then warm
+    (cached context, same scene)."""
+    times = []
+    for _ in range(3):
+        t0 = time.perf_counter()
+        rtzig.render(cam.cam, cam.scene.world, n_gpus=1, device=device)
+        times.append((time.perf_counter() - t0) * 1e3)
+    return times
 
 
 def main():
@@ -101,6 +129,7 @@ def main():
     ap.add_argument("--cpu-spp", type=int, default=4, help="spp of the bounded CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-fast", action="store_true", help="skip the f32 fast-mode side measurement")
+    ap.add_argument("--no-dropin", action="store_true", help="skip the rt_render drop-in measurement")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL over xGMI, the product) or gloo (rehearsal: several ranks on one GPU)")
     args = ap.parse_args()
@@ -163,7 +192,7 @@ def main():
         renderer.enable_profile(False)
     prof = [int(x) for x in pstats.cpu().tolist()]
     stats.zero_()
-    # HIP events around every sample / reduce launch of the timed frames, on the launch stream; read
+    # HIP events around every sample / reduce launch of the timed frames, on the launch streams; read
     # back once after the timed region, so no frame waits on the host
     renderer.enable_timing(True)
 
@@ -184,10 +213,13 @@ def main():
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed_max = float(t.item())
+    kname = renderer.kernel_name()  # the timed (parity) kernel, before the fast-mode frames
+    k_sum, _, n_launch = renderer.kernel_times_total() if n_rows else (0.0, 0.0, 0)
+    st = stats.cpu().tolist()
+    rays_per_frame = st[0] / max(1, args.steps)
+    samples_per_frame = st[1] / max(1, args.steps)
     # side measurement (1 GPU only): RT_PRECISION_F32 fast mode on the same frame.  Statistical
     # parity only (tests/test_fast_mode.py), so it is reported beside `value`, never as it.
-    kname = renderer.kernel_name()  # the timed (parity) kernel, before the fast-mode frames
-    k_sum, r_sum, _ = renderer.kernel_times_total() if n_rows else (0.0, 0.0, 0)
     fast = None
     if world == 1 and not args.no_fast and n_rows:
         renderer.set_precision("f32")
@@ -199,36 +231,40 @@ def main():
             frame()
         torch.cuda.synchronize()
         tf = (time.perf_counter() - tf0) / 2
-        fk = [renderer.kernel_times_total()[0] / 2]
         fast = {"value": round(W * H * spp / tf / 1e6, 3), "unit": "Msamples/s", "dtype": "f32",
-                "kernel": renderer.kernel_name(), "kernel_ms_avg": round(float(np.mean(fk)), 3),
+                "kernel": renderer.kernel_name(), "kernel_ms_per_frame": round(renderer.kernel_times_total()[0] / 2, 3),
                 "note": "RT_PRECISION_F32 fast mode (huge spheres in f64), statistical parity only; "
                         "not the headline value"}
         renderer.set_precision("f64")
-    st = stats.cpu().tolist()
-    rays_per_launch = st[0] / max(1, args.steps)
-    samples_per_launch = st[1] / max(1, args.steps)
+    renderer.sync()  # raises if a wave reported a hand-off timeout (never expected)
+    renderer.close()
 
     if rank == 0:
         total_samples = W * H * spp * args.steps
         value = total_samples / elapsed_max / 1e6
-        k_avg_s = k_sum / args.steps / 1e3   # sample_kernel only, per frame
-        r_avg_ms = r_sum / args.steps
-        # roofline.achieved follows the contract: ALGORITHMIC work = SURVEY §8(d)'s per-unit figure
-        # (17 FLOP per ray-sphere candidate test) x units (485 spheres x rays).  The BVH walk returns
-        # the same bits while executing ~2% of those tests, so frac can exceed 1; the work the kernel
-        # actually executes (exact counts from the instrumented frame) is reported beside it:
-        # f64 sphere tests (17 FLOP) + f32 BVH box tests (12 FLOP, counted at 1/2: f32 VALU runs at
-        # twice the f64 rate on gfx950).
-        tests, visits = prof[2], prof[3]
-        alg_tf = FLOPS_PER_TEST * n_spheres * rays_per_launch / k_avg_s / 1e12
-        exec_tf = (FLOPS_PER_TEST * tests + F32_FLOPS_PER_VISIT * visits / 2) / k_avg_s / 1e12
-        # sample_kernel HBM bytes: one 24-B f64 color per sample written (the reduce kernel reads
-        # them back: +24 B/sample, + the framebuffer)
-        alg_bytes = n_rows * W * spp * 24
-        red_bytes = n_rows * W * spp * 24 + n_rows * W * (24 if args.output == "linear" else 3)
+        launches_per_frame = n_launch / max(1, args.steps)
+        k_frame_s = k_sum / args.steps / 1e3   # sample kernel time per frame (sum of its launches)
         workload = f"final-render {W}x{H} {spp}spp depth50 ({n_spheres} spheres)"
-        traffic = pmc_traffic(workload)
+        pmc = pmc_summary(workload)
+        tests, visits = prof[2], prof[3]
+        exec_flops = FLOPS_PER_TEST * tests + F32_FLOPS_PER_VISIT * visits / 2   # f64-equivalent, per frame
+        exec_tf = exec_flops / k_frame_s / 1e12
+        alg_eq_tf = FLOPS_PER_TEST * n_spheres * rays_per_frame / k_frame_s / 1e12
+        issue = None
+        if pmc.get("valu_issue_cycles_per_frame") and pmc.get("clock_GHz"):
+            cyc = pmc["valu_issue_cycles_per_frame"]
+            issue = {"frac": round(cyc / (SIMDS * pmc["clock_GHz"] * 1e9 * k_frame_s), 4),
+                     "valu_issue_cycles_per_frame": cyc, "clock_GHz": pmc["clock_GHz"],
+                     "model": "2 cycles per wave64 32-bit VALU op, 4 per f64 add/mul/fma, 8 per "
+                              "transcendental (MI355X_MICROARCH.md), / (1024 SIMDs x clock x kernel time)",
+                     "source": pmc.get("source")}
+        # HBM: the algorithmic traffic of a frame is the f64 linear framebuffer W*H*24 (or W*H*3
+        # bytes of RGB8) written once; the rest is the design's own: each sample's
+        # 24-B color through the wave's ring (L2 / MALL when it stays there), the running sums'
+        # write-through hand-off between sample chunks (24 B per pixel per chunk, both ways)
+        alg_bytes = n_rows * W * (24 if args.output == "linear" else 3)
+        frame_ms = elapsed_max / args.steps * 1e3
+        traffic = pmc.get("hbm_bytes_per_frame")
         assert img is not None and img.shape[0] == H
         res = {
             "metric": METRIC,
@@ -237,7 +273,7 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": round(elapsed_max / args.steps * 1e3, 3),
+            "ms_per_step": round(frame_ms, 3),
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
@@ -250,55 +286,57 @@ def main():
                            + ("RCCL gather to rank 0" if args.dist_backend == "nccl" else
                               "gloo gather to rank 0 (rehearsal: ranks share devices)")},
             "roofline": {
-                # compute roofline ("mfma" in the bench contract): this path has no GEMM, its f64
-                # work runs on the VALU, and MI355X's dense FP64 peak is 78.6 TF/s for the vector
-                # and the matrix pipe alike, so the compute ceiling is the same number
-                "bound": "mfma",
-                "pipe": "f64 VALU (no GEMM-shaped work on this path)",
+                "bound": "valu",
                 "kernel": kname,
-                "achieved": round(alg_tf, 3),
+                "achieved": round(exec_tf, 3),
                 "peak": FP64_VALU_PEAK_TFLOPS,
                 "unit": "TFLOP/s",
-                "frac": round(alg_tf / FP64_VALU_PEAK_TFLOPS, 4),
+                "frac": round(exec_tf / FP64_VALU_PEAK_TFLOPS, 4),
                 "traffic": traffic,
-                "work": f"algorithmic (SURVEY §8(d)): {FLOPS_PER_TEST} FLOP x {n_spheres} spheres x "
-                        f"{rays_per_launch:.0f} rays per launch (rank 0, {n_rows} rows)",
-                "executed": {
-                    "achieved": round(exec_tf, 3),
-                    "frac": round(exec_tf / FP64_VALU_PEAK_TFLOPS, 4),
-                    "sphere_tests_per_ray": round(tests / max(1, prof[0]), 3),
-                    "node_visits_per_ray": round(visits / max(1, prof[0]), 3),
-                    "note": "FLOPs the kernel executes: exact f64 sphere tests x 17 + f32 BVH box tests "
-                            "x 12 at 1/2 weight; the BVH walk is bound by VALU issue under SIMT "
-                            "divergence, not by FLOPs (DESIGN.md §5)",
-                },
-                "kernel_ms_avg": round(k_avg_s * 1e3, 3),
-                "reduce_kernel_ms_avg": round(r_avg_ms, 3),
+                "work": f"executed per frame (rank 0, {n_rows} rows; exact counts of one instrumented frame): "
+                        f"{tests} f64 ray-sphere tests x {FLOPS_PER_TEST} FLOP (SURVEY §8(d) unit) + "
+                        f"{visits} BVH node visits x {F32_FLOPS_PER_VISIT} f32 FLOP at 1/2 weight = "
+                        f"{exec_flops:.4g} FLOP / {k_frame_s * 1e3:.3f} ms of sample kernel",
+                "sphere_tests_per_ray": round(tests / max(1, prof[0]), 3),
+                "node_visits_per_ray": round(visits / max(1, prof[0]), 3),
+                "issue": issue,
+                "algorithmic_equivalent": {
+                    "TFLOP/s": round(alg_eq_tf, 3),
+                    "note": f"SURVEY §8(d)'s list-walk work {FLOPS_PER_TEST} x {n_spheres} spheres x "
+                            f"{rays_per_frame:.0f} rays per frame: the BVH returns the same bits while "
+                            "executing ~1% of those tests, so this is not a roofline fraction"},
+                "kernel_ms_per_frame": round(k_frame_s * 1e3, 3),
+                "launches_per_frame": round(launches_per_frame, 3),
+                "kernel_ms_avg": round(k_frame_s * 1e3 / max(1.0, launches_per_frame), 3),
             },
             "hbm": {
-                "kernel": "sample_kernel (per-sample color stores)",
-                "algorithmic_bytes_per_launch": alg_bytes,
-                "achieved_GBps": round(alg_bytes / k_avg_s / 1e9, 3),
+                "algorithmic_bytes_per_frame": alg_bytes,
+                "achieved_GBps": round(alg_bytes / (frame_ms / 1e3) / 1e9, 3),
                 "peak_GBps": HBM_PEAK_GBS,
-                "frac": round(alg_bytes / k_avg_s / 1e9 / HBM_PEAK_GBS, 6),
-                # the ordered per-pixel reduction is the HBM-bound kernel of the path: it reads every
-                # per-sample color once and writes the framebuffer
-                "reduce_kernel": {
-                    "algorithmic_bytes_per_launch": red_bytes,
-                    "achieved_GBps": round(red_bytes / (r_avg_ms / 1e3) / 1e9, 1) if r_avg_ms > 0 else None,
-                    "frac": round(red_bytes / (r_avg_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4) if r_avg_ms > 0 else None,
-                },
+                "frac": round(alg_bytes / (frame_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 7),
+                "pmc_bytes_per_frame": traffic,
+                "traffic_over_algorithmic": round(traffic / alg_bytes, 1) if traffic else None,
+                "overhead": "the in-kernel ordered accumulation: each sample's 24-B color written to and read "
+                            "back from its wave's ring (an upper bound of "
+                            f"{n_rows * W * spp * 48 / 1e9:.2f} GB per frame if none of it stays in L2 / MALL), "
+                            "and the running sums' write-through hand-off, 48 B per pixel per sample chunk",
             },
-            "rays_per_sample": round(rays_per_launch / max(1, samples_per_launch), 4),
+            "rays_per_sample": round(rays_per_frame / max(1, samples_per_frame), 4),
             "fixed_costs_ms": {"context_and_scene_upload": round(init_ms, 2)},
             "cpu_baseline": None,
             "fast_f32": fast,
         }
+        if world == 1 and not args.no_dropin and n_rows:
+            times = dropin(cam, local_dev)
+            res["dropin_ms"] = {"cold": round(times[0], 2), "warm": round(min(times[1:]), 2),
+                                "warm_over_frame": round(min(times[1:]) / frame_ms, 4),
+                                "note": "rt_render(n_gpus=1) into host memory (f64 linear): cold = first call of "
+                                        "the process (context, scene + BVH upload, workspace, render, D2H); "
+                                        "warm = cached context, same scene"}
         if world == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(W, args.aspect, args.cpu_spp)
             res["speedup_vs_cpu_baseline"] = round(value / res["cpu_baseline"]["value"], 1)
         print(json.dumps(res), flush=True)
-    renderer.close()
     if world > 1:
         dist.destroy_process_group()
 

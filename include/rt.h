@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 2
+#define RT_ABI_VERSION 3
 
 /* ---- status codes ---------------------------------------------------------------------------- */
 typedef enum rt_status {
@@ -107,9 +107,16 @@ typedef struct rt_options {
 
 /* ---- the drop-in: Camera.render() ------------------------------------------------------------ */
 /* Renders the whole image into host memory `out` (row-major, j*W+i).  LINEAR_F64: W*H pixels of
- * `pixel_stride` doubles (first 3 are r,g,b); RGB8: W*H*3 bytes.  Blocks the calling thread.      */
+ * `pixel_stride` doubles (first 3 are r,g,b); RGB8: W*H*3 bytes.  Blocks the calling thread.
+ * The library keeps one device context per GPU for the life of the process (created on first use,
+ * on parallel host threads): a later call on the same sphere list re-uploads and rebuilds nothing.
+ * Its workspace is fixed per device: ≈ 0.8 GB of wave rings plus 24 B per pixel (no per-sample
+ * buffer: the kernel accumulates every pixel's samples in order itself).  Calls are serialised by
+ * an internal lock.                                                                               */
 int rt_render(const rt_camera* cam, const rt_sphere* spheres, size_t n_spheres,
               const rt_options* opts, void* out);
+/* Frees rt_render's cached device contexts (optional; the next rt_render creates them again). */
+int rt_release_cached_contexts(void);
 
 /* ---- device-resident path (bench / multi-process drivers) ------------------------------------ */
 typedef struct rt_context rt_context;
@@ -120,25 +127,32 @@ int rt_context_destroy(rt_context* ctx);
 int rt_context_set_scene(rt_context* ctx, const rt_sphere* spheres, size_t n_spheres);
 /* Renders rows j = row0 + k*row_step, k in [0, n_rows), into DEVICE memory `d_out`
  * (n_rows*W pixels; LINEAR_F64 stride 3 doubles, or RGB8) on HIP stream `stream` (NULL = default).
- * Asynchronous: returns after the launch.  `d_stats` (device, 2 x uint64, may be NULL) is
- * atomically incremented with {rays, samples}. */
+ * Asynchronous: returns after the launches; the output is complete when `stream` reaches the point
+ * of the call.  `d_stats` (device, 2 x uint64, may be NULL) is atomically incremented with
+ * {rays, samples}.  One kernel launch per call.  A context is not re-entrant: calls on one context
+ * must come from one host thread at a time; a call on a different stream than the previous one
+ * waits for the previous call's work, and scene changes / buffer growth wait for it on the host. */
 int rt_render_rows_async(rt_context* ctx, const rt_camera* cam, uint32_t output_format,
                          uint32_t row0, uint32_t row_step, uint32_t n_rows,
                          void* d_out, void* d_stats, void* stream);
+/* Waits for the context's last render and reports a failure the kernel recorded (RT_ERR_HIP: a
+ * wave gave up waiting for a running-sum hand-off — a bug guard, never expected). */
+int rt_context_sync(rt_context* ctx);
 /* Arithmetic of the context's later renders: rt_precision (default RT_PRECISION_F64).  F32 needs
  * the BVH walk (any scene whose BVH builds); otherwise the parity kernel runs. */
 int rt_context_set_precision(rt_context* ctx, int precision);
 /* Name of the kernel variant the context launches (for profiling / logs). */
 const char* rt_kernel_name(rt_context* ctx);
-/* Optional per-kernel timing with HIP events recorded on the launch stream around every sample and
- * reduce kernel of a render call.  rt_context_kernel_times waits for the last event and returns the
- * summed durations (ms) of the most recent rt_render_rows_async call. */
+/* Optional kernel timing with HIP events recorded on the launch stream around the sample kernel of
+ * every render call.  rt_context_kernel_times waits for the last event and returns the duration
+ * (ms) of the most recent rt_render_rows_async call; *reduce_ms is 0 (there is no reduce pass since
+ * ABI 3: the sample kernel accumulates in sample order itself). */
 int rt_context_enable_timing(rt_context* ctx, int enable);
 int rt_context_kernel_times(rt_context* ctx, double* sample_ms, double* reduce_ms);
-/* The same summed over every chunk of every call since timing was (re)enabled (at most 1024 chunks;
- * beyond that the totals restart), so a caller can time many frames without a host sync per frame.
- * *n_chunks = the number of sample-kernel launches summed. */
-int rt_context_kernel_times_total(rt_context* ctx, double* sample_ms, double* reduce_ms, uint32_t* n_chunks);
+/* The same summed over every call since timing was (re)enabled (at most 1024 calls; beyond that the
+ * totals restart), so a caller can time many frames without a host sync per frame.
+ * *n_launches = the number of sample-kernel launches summed. */
+int rt_context_kernel_times_total(rt_context* ctx, double* sample_ms, double* reduce_ms, uint32_t* n_launches);
 /* Instrumented kernels (diagnostics): when enabled, `d_stats` of rt_render_rows_async must hold 24
  * uint64: {rays, samples, sphere tests executed, BVH node visits, wave-cycles in queue refill,
  * wave-cycles in the closest-hit walk, wave-cycles in shading, wave-iterations of the BVH inner

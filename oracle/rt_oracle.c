@@ -562,6 +562,54 @@ EXPORT void oracle_refract(const double* v, const double* n, double eta, double*
  * red sphere (0,0,-1) r 0.5 hit when disc >= 0 (sphere.zig:27-33 without the root test); colors
  * quantised as trunc(255.999 * c) with no gamma.  Byte-exact vs both fixtures (tests/test_oracle.py).
  * ---------------------------------------------------------------------------------------------- */
+/* Chapters 6/7 (test-files/chapter6.ppm, chapter7.ppm — BASELINE config 1's "normals" variant):
+ * the same camera, world = sphere (0,0,-1) r 0.5 + ground (0,-100.5,-1) r 100 walked like
+ * HittableList.hit (hittable.zig:64-77) over Sphere.hit (sphere.zig:26-54) on the interval
+ * (0, inf); a hit shades 0.5 * (normal + (1,1,1)) with the face-forward normal (sphere.zig:45-53).
+ * Chapter 6 quantises trunc(255.999 * c); chapter 7 trunc(256 * clamp(c, 0, 0.999))
+ * (Interval.clamp interval.zig:40-47, as Color.toRgb color.zig:63-76 without the gamma). */
+static int book_hit(v3 o, v3 d, double t_min, v3* nrm) {
+    static const double cs[2][4] = {{0, 0, -1, 0.5}, {0, -100.5, -1, 100}};
+    double closest = INFINITY;
+    int found = 0;
+    for (int k = 0; k < 2; k++) {
+        const v3 c = V(cs[k][0], cs[k][1], cs[k][2]);
+        const double r = cs[k][3];
+        const v3 oc = sub(c, o);
+        const double a = len_sq(d), h = dot(d, oc), cc = len_sq(oc) - r * r;
+        const double disc = h * h - a * cc;
+        if (disc < 0) continue;
+        const double sq = sqrt(disc);
+        double root = (h - sq) / a;
+        if (!(t_min < root && root < closest)) {
+            root = (h + sq) / a;
+            if (!(t_min < root && root < closest)) continue;
+        }
+        closest = root;
+        const v3 p = add(o, muls(d, root));
+        const v3 out = divs(sub(p, c), r);
+        *nrm = dot(d, out) < 0 ? out : neg(out);
+        found = 1;
+    }
+    return found;
+}
+
+static v3 book_color(int chapter, v3 center, v3 d) {
+    if (chapter == 5) {
+        const v3 oc = sub(V(0, 0, -1), center);
+        const double a = len_sq(d), hh = dot(d, oc), c = len_sq(oc) - 0.5 * 0.5;
+        if (hh * hh - a * c >= 0) return V(1, 0, 0);
+    }
+    v3 nrm;
+    if ((chapter == 6 || chapter == 7) && book_hit(center, d, 0.0, &nrm)) return muls(add(nrm, V(1, 1, 1)), 0.5);
+    const double a = 0.5 * (unit(d).y + 1.0);
+    return add(muls(V(1, 1, 1), 1.0 - a), muls(V(0.5, 0.7, 1), a));
+}
+
+/* Chapter 7 is the chapter-6 scene antialiased (the book's camera class): `spp` jittered samples
+ * per pixel (sampleSquare camera.zig:203-209), averaged, quantised trunc(256 * clamp(c, 0, 0.999)).
+ * Its RNG stream is unknown (the fixture predates src/), so it is compared statistically; the
+ * jitter here draws from DefaultPrng.init(1). */
 EXPORT int oracle_render_book(int chapter, uint32_t width, double ratio, uint8_t* rgb, uint32_t* height_out) {
     size_t h = (size_t)((double)width / ratio);
     if (h < 1) h = 1;
@@ -572,27 +620,36 @@ EXPORT int oracle_render_book(int chapter, uint32_t width, double ratio, uint8_t
     const v3 du = divs(vu, W), dv = divs(vv, H);
     const v3 ul = sub(sub(sub(center, V(0, 0, 1.0)), divs(vu, 2)), divs(vv, 2));
     const v3 p00 = add(ul, muls(add(du, dv), 0.5));
+    const int spp = chapter == 7 ? 100 : 1;
+    xoshiro g;
+    xoshiro_seed(&g, 1);
     for (size_t j = 0; j < h; j++) {
         for (uint32_t i = 0; i < width; i++) {
-            const v3 pc = add(add(p00, muls(du, (double)i)), muls(dv, (double)j));
-            const v3 d = sub(pc, center);
             v3 col;
-            int hit = 0;
-            if (chapter == 5) {
-                const v3 oc = sub(V(0, 0, -1), center);
-                const double a = len_sq(d), hh = dot(d, oc), c = len_sq(oc) - 0.5 * 0.5;
-                hit = hh * hh - a * c >= 0;
-            }
-            if (hit) {
-                col = V(1, 0, 0);
+            if (spp == 1) {
+                const v3 pc = add(add(p00, muls(du, (double)i)), muls(dv, (double)j));
+                col = book_color(chapter, center, sub(pc, center));
             } else {
-                const double a = 0.5 * (unit(d).y + 1.0);
-                col = add(muls(V(1, 1, 1), 1.0 - a), muls(V(0.5, 0.7, 1), a));
+                col = V(0, 0, 0);
+                for (int s = 0; s < spp; s++) {
+                    const double ox = rd(&g) - 0.5, oy = rd(&g) - 0.5;
+                    const v3 pc = add(add(p00, muls(du, (double)i + ox)), muls(dv, (double)j + oy));
+                    col = add(col, book_color(chapter, center, sub(pc, center)));
+                }
+                col = muls(col, 1.0 / spp);
             }
             uint8_t* o = rgb + 3 * (j * width + i);
-            o[0] = (uint8_t)(int)(255.999 * col.x);
-            o[1] = (uint8_t)(int)(255.999 * col.y);
-            o[2] = (uint8_t)(int)(255.999 * col.z);
+            if (chapter == 7) {
+                const double cl[3] = {col.x, col.y, col.z};
+                for (int k = 0; k < 3; k++) {
+                    const double x = cl[k] < 0.0 ? 0.0 : (cl[k] > 0.999 ? 0.999 : cl[k]);
+                    o[k] = (uint8_t)(int)(256.0 * x);
+                }
+            } else {
+                o[0] = (uint8_t)(int)(255.999 * col.x);
+                o[1] = (uint8_t)(int)(255.999 * col.y);
+                o[2] = (uint8_t)(int)(255.999 * col.z);
+            }
         }
     }
     if (height_out) *height_out = (uint32_t)h;

@@ -71,18 +71,6 @@ struct Builder {
         }
     }
 
-    // SAH weight of a side holding n prims: n (the classic count), or with RTZIG_BVH_SAH_LEAVES=1
-    // the number of kLeafMax-slot leaves it needs, ceil(n / kLeafMax): every leaf costs one padded
-    // leaf round whether it holds 1 or kLeafMax spheres
-    int sah_leaves = -1;
-    double leaf_weight(size_t n) {
-        if (sah_leaves < 0) {
-            const char* e = std::getenv("RTZIG_BVH_SAH_LEAVES");
-            sah_leaves = e ? std::atoi(e) : 0;
-        }
-        return sah_leaves ? (double)((n + kLeafMax - 1) / kLeafMax) : (double)n;
-    }
-
     // Leaves are padded to exactly kLeafMax slots with sentinels (kSentinel: never-hit geometry,
     // see rt_kernel.h), so the kernel tests every leaf with one fixed, unrolled block.
     int32_t leaf(size_t b, size_t e) {
@@ -126,7 +114,7 @@ struct Builder {
             double lo[3], hi[3];
             for (int a = 0; a < 3; a++) { lo[a] = prims[b].lo[a]; hi[a] = prims[b].hi[a]; }
             for (size_t i = b + 1; i < e; i++) {
-                left_area[i - b] = area(lo, hi) * leaf_weight(i - b);
+                left_area[i - b] = area(lo, hi) * (double)(i - b);
                 for (int a = 0; a < 3; a++) {
                     lo[a] = std::min(lo[a], prims[i].lo[a]);
                     hi[a] = std::max(hi[a], prims[i].hi[a]);
@@ -134,7 +122,7 @@ struct Builder {
             }
             for (int a = 0; a < 3; a++) { lo[a] = prims[e - 1].lo[a]; hi[a] = prims[e - 1].hi[a]; }
             for (size_t i = e - 1; i > b; i--) {
-                const double cost = left_area[i - b] + area(lo, hi) * leaf_weight(e - i);
+                const double cost = left_area[i - b] + area(lo, hi) * (double)(e - i);
                 if (cost < best_cost) {
                     best_cost = cost;
                     best_axis = ax;

@@ -193,10 +193,6 @@ struct Rng {
 
     // DefaultPrng.init(key): Xoshiro256.seed via SplitMix64 (zig std/Random/Xoshiro256.zig)
     __device__ __forceinline__ void seed(uint64_t key) {
-#ifdef RTZIG_ABLATE_SEED  // timing ablation only: no SplitMix64 seeding
-        s0 = key; s1 = key ^ 0x1234567887654321ULL; s2 = ~key; s3 = key ^ 0x0f0f0f0ff0f0f0f0ULL;
-        return;
-#endif
         uint64_t sm = key;
         s0 = splitmix_next(sm);
         s1 = splitmix_next(sm);
@@ -267,35 +263,6 @@ struct Rng {
 // hoisted to the host.  For a fixed seed the map (pixel, sample) -> key is a bijection.
 __device__ __forceinline__ uint64_t sample_key(uint64_t seed_mix, uint64_t pixel, uint32_t sample) {
     return sm_mix_hd(seed_mix ^ ((pixel << 32) | (uint64_t)sample));
-}
-
-// Work-queue claim size (guided self-scheduling): a wave claims kChunk items while plenty remain
-// and ever smaller chunks as its queue segment drains, so waves run out of work within a few path
-// lengths of each other.  `seen` = an estimate of the segment's position, `nwaves` = waves
-// claiming from it.  A claim takes 1/K of an even share of what is left, (remaining / nwaves) / K,
-// with K = 8 and a floor of 64 items (1 per lane).  A/B (tools/gpu_abchunk.sh,
-// profiles/r01_chunk): K = 2 -> 8 cut the kernel 6% on rank 0's rows of an 8-GPU job and 1% on the
-// whole final frame and on chapter 13; K >= 12 is slower.  With ONE queue counter a floor below
-// 256 cost the short chapter 9 frame up to 45% (each claim is an atomic on that one address);
-// with 8 counters (rtk::kQueues) the 64-item floor is the fastest on every config.
-#ifndef RTZIG_GUIDED
-#define RTZIG_GUIDED 1
-#endif
-#ifndef RTZIG_GUIDED_K
-#define RTZIG_GUIDED_K 8
-#endif
-#ifndef RTZIG_MIN_CHUNK
-#define RTZIG_MIN_CHUNK 64
-#endif
-__device__ __forceinline__ uint64_t guided_chunk(uint64_t total, uint64_t seen, uint64_t nwaves, uint64_t max_chunk) {
-#if RTZIG_GUIDED
-    const uint64_t rem = total > seen ? total - seen : 0;
-    uint64_t c = (rem / (RTZIG_GUIDED_K * nwaves)) & ~63ull;
-    return c < RTZIG_MIN_CHUNK ? RTZIG_MIN_CHUNK : (c > max_chunk ? max_chunk : c);
-#else
-    (void)total; (void)seen; (void)nwaves;
-    return max_chunk;
-#endif
 }
 
 // std.math.pow(f64, x, 5) for x in [0, 2] (frexp + repeated squaring == x*((x*x)*(x*x)))

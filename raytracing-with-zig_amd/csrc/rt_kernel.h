@@ -11,69 +11,65 @@ namespace rtk {
 
 constexpr int kBlock = 256;                // 4 waves of 64 lanes
 constexpr uint32_t kMaxLdsSpheres = 2048;  // 64 KiB of LDS geometry; above this, read from global
-#ifndef RTZIG_CHUNK
-#define RTZIG_CHUNK 2048
-#endif
-constexpr uint32_t kChunk = RTZIG_CHUNK;          // work items a wave claims per queue fetch (at most: guided_chunk)
-#ifndef RTZIG_QUEUE_HOME
-#define RTZIG_QUEUE_HOME 0  // 1: segment (block / kQueues) % kQueues (A/B knob)
-#endif
-#ifndef RTZIG_QUEUES
-#define RTZIG_QUEUES 8
-#endif
-// Work-queue counters: the items of a launch are split into kQueues contiguous segments, one
-// counter each (kQueueStride u64 apart, separate 256-B lines); a wave claims from the segment of
-// its block (blockIdx % kQueues) and moves on to the next segments once that one is exhausted.
-// One counter serves ~88 claims per µs; 8 of them let the claims shrink to 64 items at the end of a
-// launch (A/B, profiles/r01_chunk: chapter 9 -8%, rank 0's N = 8 rows -1%, final frame -0.5%).
-constexpr uint32_t kQueues = RTZIG_QUEUES;
-constexpr uint32_t kQueueStride = 32;
-constexpr size_t kQueueBytes = (size_t)kQueues * kQueueStride * sizeof(unsigned long long);
-constexpr size_t kQueueBufferBytes = 4096;  // allocated by rt_runtime.cpp
-static_assert(kQueues >= 1 && kQueueBytes <= kQueueBufferBytes, "queue counters exceed the queue buffer");
-// Wave-uniform claim state of the segmented work queue (path_loop, path_loop_fast).  claim()
-// fetches a new window [cur, end) of item numbers: a guided claim from the wave's current segment,
-// sized from an estimate of that segment's position (this wave's previous claim plus one such claim
-// by every other wave of the segment since, rtk::guided_chunk); an exhausted segment sends the wave
-// on to the next one, where it claims RTZIG_MIN_CHUNK items at a time.  After kQueues failed claims
-// (one per segment) it returns false for good, so every wave reaches the drained state.
-struct WorkQueue {
-    uint64_t total, seg_waves;
-    uint64_t cur = 0, end = 0, qend = 0, last_chunk = 0;
-    uint32_t qcur, qmoves = 0;
-    __device__ WorkQueue(uint64_t total_, uint64_t nwaves, uint32_t block)
-        : total(total_), seg_waves(nwaves / kQueues > 0 ? nwaves / kQueues : 1),
-          qcur(kQueues == 1 ? 0 : (RTZIG_QUEUE_HOME ? block / kQueues : block) % kQueues) {}
-    __device__ __forceinline__ bool claim(unsigned long long* __restrict__ queue, uint32_t lane) {
-        while (qmoves < kQueues) {
-            const uint32_t q = qcur;
-            const uint64_t s0 = kQueues == 1 ? 0 : total * q / kQueues;
-            const uint64_t s1 = kQueues == 1 ? total : total * (q + 1) / kQueues;
-            const uint64_t chunk = qmoves == 0 ? guided_chunk(s1 - s0, qend + seg_waves * last_chunk, seg_waves, kChunk)
-                                               : (uint64_t)RTZIG_MIN_CHUNK;
-            last_chunk = chunk;
-            unsigned long long base = 0;
-            if (lane == 0) base = atomicAdd(queue + (size_t)q * kQueueStride, (unsigned long long)chunk);
-            base = __shfl(base, 0, 64);
-            if (base < s1 - s0) {
-                qend = base + chunk < s1 - s0 ? base + chunk : s1 - s0;
-                cur = s0 + base;
-                end = s0 + qend;
-                return true;
-            }
-            ++qmoves;
-            qcur = qcur + 1 == kQueues ? 0 : qcur + 1;
-        }
-        return false;
-    }
+// ------------------------------------------------------------------------------------------------
+// Work units and the ordered in-kernel accumulation.
+//
+// The reference sums a pixel's samples strictly in sample order (camera.zig:133-136:
+// pixelColor += rayColor(ray), then * pixelSamplesScale at :137), so the f64 result depends on that
+// order.  A work UNIT is (tile, chunk): the 64 consecutive pixels q = 64 * tile + l (l = 0..63) of
+// the launch's rows x the samples [s0, s0 + S) of chunk k.  Units are claimed from one counter in
+// chunk-major order (all tiles' chunk 0, then chunk 1, ...), so the 64 lanes of a wave trace
+// neighbouring pixels.  A wave holds up to kSlots units at once and hands their S x 64 items to its
+// lanes in sample-major order (item m: sample s0 + m / 64 of pixel 64 * tile + m % 64); a lane whose
+// path ends stores its color into the unit's slot of the wave's private ring [slot][m][3] and takes
+// the next item.  When every item of a unit has ended, the wave FINALISES it: lane l adds the ring's
+// S colors of pixel l, in sample order, to the pixel's running sum — after the unit of the previous
+// chunk of the same tile has been finalised (per-tile flag) — and writes the sum back (write-through
+// sc1 stores, drained, then the flag: MI355X hand-off recipe, any XCD), or, for the last chunk,
+// writes the framebuffer (scale + optional Color.toRgb).  No per-sample buffer and no reduce pass.
+// Chunks: kUnitS samples each, then a halving tail down to 1 sample (fine-grained units while the
+// frame drains): R = spp - n_main * kUnitS in [kUnitS, 2 kUnitS) (or spp if smaller), tail chunk t
+// covers [R - rem(t), R - rem(t + 1)) with rem(t) = ceil(R / 2^t), rem(T + 1) = 0, 2^T >= R.
+// ------------------------------------------------------------------------------------------------
+constexpr uint32_t kUnitS = 16;   // samples per unit of the main chunks
+constexpr uint32_t kSlots = 4;    // units a wave holds at once
+constexpr uint32_t kSlotMask = (1u << kSlots) - 1;
+constexpr uint32_t kRingSlotDoubles = kUnitS * 64 * 3;
+constexpr uint32_t kRingWaveDoubles = kSlots * kRingSlotDoubles;  // 96 KiB of f64 per wave
+constexpr size_t kCtrBytes = 256;  // [0] unit claim counter, [8] error word (zeroed per launch)
+
+struct UnitArgs {
+    double* ring;              // [waves][kSlots][kUnitS * 64][3] wave-private sample colors
+    double* sums;              // [P][3] running per-pixel sums (write-through hand-off between waves)
+    uint32_t* flags;           // [n_tiles] chunks finalised per tile (zeroed per launch)
+    void* out;                 // [P][3] f64 linear or u8 RGB (the last chunk's finalisation)
+    unsigned long long* ctr;   // kCtrBytes: [0] claim counter, [8] error word
+    FastDiv div_tiles;         // u -> (chunk, tile)
+    uint32_t n_tiles, n_units; // n_units = n_tiles * n_chunks < 2^32
+    uint32_t n_main, tail_r;   // main chunks of kUnitS samples; tail length R
+    uint32_t tail_t, n_chunks; // 2^tail_t >= R; n_chunks = n_main + tail_t + 1
+    uint32_t P, out_format;    // pixels of the launch; 0 linear f64, 1 rgb8
+    uint32_t ring_waves, pad;  // ring capacity in waves (the launch never has more)
+    double scale;              // pixelSamplesScale
 };
+
+// samples [*s0, *s0 + *n) of chunk k
+__host__ __device__ inline void chunk_range(const UnitArgs& u, uint32_t k, uint32_t* s0, uint32_t* n) {
+    if (k < u.n_main) {
+        *s0 = k * kUnitS;
+        *n = kUnitS;
+        return;
+    }
+    const uint32_t t = k - u.n_main, R = u.tail_r;
+    const uint32_t rem = (R + (1u << t) - 1) >> t;
+    const uint32_t rem1 = t < u.tail_t ? (R + (2u << t) - 1) >> (t + 1) : 0u;
+    *s0 = u.n_main * kUnitS + (R - rem);
+    *n = rem - rem1;
+}
 
 constexpr uint32_t kPad = 4;               // sphere list padded to a multiple of this (sentinels)
 #ifndef RTZIG_RUV_TRIPS
 #define RTZIG_RUV_TRIPS 3
-#endif
-#ifndef RTZIG_TRIP_DEFER
-#define RTZIG_TRIP_DEFER 0  // >0: skip trips 2.. when at most this many lanes still need a draw
 #endif
 constexpr int kRuvTrips = RTZIG_RUV_TRIPS;  // randomUnitVec rejection trips per loop iteration (path_loop)
 constexpr const char* kDefaultVariant = "smem_u4";  // see variant_choice() in rt_kernel.hip
@@ -112,10 +108,9 @@ struct KernelParams {
     uint64_t seed_mix;  // sm_mix(seed), hoisted from sample_key
     uint32_t row0, row_step, n_rows, n_spheres;
     uint32_t n_pad;  // n_spheres rounded up to kPad (sentinel-padded)
-    uint32_t s_begin, s_count;
+    uint32_t s_begin, s_count;  // unused by the unit scheduler (kept for the kernarg layout)
     uint32_t prof;   // 1: instrumented build, stats has 8 entries (see rt_context_enable_profile)
-    uint32_t order;  // work-item order: 0 sample-major, 1 pixel-major, 2 sample-major over 8x8 tiles (RTZIG_ORDER)
-    uint32_t pad2;
+    uint32_t pad2[2];
     FastDiv div_layer;  // / (n_rows * width): item -> (sample, pixel) in the refill
     FastDiv div_width;  // / width: pixel -> (row, column)
     // f32 copies of the camera constants for the fast (RT_PRECISION_F32) kernel, read by scalar
@@ -136,9 +131,6 @@ constexpr int kBlockBvh = 512;     // 8 waves; 2 blocks per CU share the LDS bud
 constexpr int kMaxDepthBvh = 16;   // == rtbvh::kMaxDepth: bound on per-lane LDS stack entries (entry 0: "done")
 #ifndef RTZIG_LEAF
 #define RTZIG_LEAF 2
-#endif
-#ifndef RTZIG_LEAF_FILTER
-#define RTZIG_LEAF_FILTER 1  // 0: every slot with disc >= 0; 1: drop spheres behind; 2: also beyond closest
 #endif
 constexpr int kLeafBvh = RTZIG_LEAF;       // == rtbvh::kLeafMax: slots per (sentinel-padded) leaf
 struct alignas(8) BvhNode {
@@ -161,37 +153,31 @@ struct BvhArgs {
     const uint32_t* always_sid;
     uint32_t n_nodes, n_leaves, n_always;
     uint32_t stack_depth;  // per-lane stack entries the tree needs: its depth (root = 1), <= kMaxDepthBvh
+    // The f32 box padding covers ray origins with max|o_i| <= the builder's origin bound; this is
+    // that bound rounded down to f32.  A lane whose f32 origin lies beyond it (a secondary ray
+    // leaving an unboundable always-list sphere far out) takes no box culling: it visits every leaf.
+    float origin_bound;
+    uint32_t pad;
 };
 // LDS layout of the BVH kernel: [nodes, padded to 16 B][leaves][stacks: stack_depth x kBlockBvh x 4 B]
 __host__ __device__ inline uint32_t bvh_leaves_offset(uint32_t n_nodes) {
     return (n_nodes * (uint32_t)sizeof(BvhNode) + 15u) & ~15u;
 }
 
-// Arguments of the ordered reduction: pixel q's running sum += samples[s][q] for s = 0..s_count-1
-// (exactly the reference's sequential `pixelColor += rayColor(ray)`, camera.zig:133-136).
-struct ReduceParams {
-    uint32_t n_pixels, s_count;
-    uint32_t first, last;   // first chunk starts from 0; last chunk scales and writes the output
-    uint32_t out_format;    // 0 linear f64 (3 doubles per pixel), 1 rgb8
-    uint32_t pad;
-    double scale;
-};
-
 }  // namespace rtk
 
-// Launch wrappers (rt_kernel.hip); all asynchronous on `stream`.
+// Launch wrappers (rt_kernel.hip, rt_kernel_fast.hip); asynchronous on `stream`.  The caller zeroes
+// ua->ctr (kCtrBytes) and ua->flags (n_tiles x 4 B) before every launch.
 extern "C" hipError_t rtk_launch_samples(const rtk::KernelParams* p, const rtk::GeoRec* geo,
-                                         const rtk::MatRec* mat, double* samples, void* queue,
+                                         const rtk::MatRec* mat, const rtk::UnitArgs* ua,
                                          void* stats, hipStream_t stream, const char** name);
 extern "C" hipError_t rtk_launch_samples_bvh(const rtk::KernelParams* p, const rtk::BvhArgs* b,
-                                             const rtk::GeoRec* geo, const rtk::MatRec* mat, double* samples,
-                                             void* queue, void* stats, hipStream_t stream, const char** name);
-extern "C" hipError_t rtk_launch_reduce(const rtk::ReduceParams* p, const double* samples,
-                                        double* sums, void* out, hipStream_t stream);
+                                             const rtk::GeoRec* geo, const rtk::MatRec* mat, const rtk::UnitArgs* ua,
+                                             void* stats, hipStream_t stream, const char** name);
 // Fast mode (rt_kernel_fast.hip): the same persistent path loop and BVH in f32 arithmetic, with
 // the always-list (huge / unboundable) spheres tested in f64.  Statistical parity only.
 extern "C" hipError_t rtk_launch_samples_fast(const rtk::KernelParams* p, const rtk::BvhArgs* b, const rtk::GeoRec* geo,
-                                              const rtk::MatRec* mat, double* samples, void* queue, void* stats,
+                                              const rtk::MatRec* mat, const rtk::UnitArgs* ua, void* stats,
                                               hipStream_t stream, const char** name);
 // Resident blocks of `kernel` on the current device (CUs x occupancy), cached (rt_kernel.hip).
 extern "C" hipError_t rtk_resident_blocks(const void* kernel, int block, size_t shmem, uint32_t* blocks);

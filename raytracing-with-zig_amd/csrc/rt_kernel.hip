@@ -36,6 +36,7 @@
 
 #include "rt_device.h"
 #include "rt_kernel.h"
+#include "rt_units.h"
 
 #pragma clang fp contract(off)
 
@@ -278,22 +279,19 @@ __device__ __forceinline__ uint32_t lds_addr(const void* p) {
     return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
 }
 
-// Exact candidate filters for the leaf round (RTZIG_LEAF_FILTER >= 1).  With s = fl(sqrt(disc)),
-// the reference's roots are root1 = fl(fl(h - s) / a) <= root2 = fl(fl(h + s) / a), and the
-// candidate of a sphere is root1 if t_min < root1, else root2 if t_min < root2 (sphere.zig:35-41).
-//   behind(h, disc):            proves root2 <= t_min, so the sphere yields no candidate;
-//   beyond(h, disc, closest):   proves root1 > closest, so its candidate (>= root1) cannot win, not
-//                               even by the lower-index tie rule.
-// Both are evaluated with explicit fma and margins of 2^-30 relative (plus a * 2^-600 absolute)
-// that dominate every rounding error of the comparison (a few ulps), so neither ever rejects a
-// sphere the exact candidate() would accept; NaN or inf operands make the tests false (keep the
-// sphere).  Proof for behind (beyond is symmetric): Z = (t_min*a - margins) - h - 2^-30|h|;
+// Exact candidate filter for the leaf round.  With s = fl(sqrt(disc)), the reference's roots are
+// root1 = fl(fl(h - s) / a) <= root2 = fl(fl(h + s) / a), and the candidate of a sphere is root1 if
+// t_min < root1, else root2 if t_min < root2 (sphere.zig:35-41).  behind(h, disc) proves
+// root2 <= t_min, so the sphere yields no candidate.  It is evaluated with explicit fma and margins
+// of 2^-30 relative (plus a * 2^-600 absolute) that dominate every rounding error of the comparison
+// (a few ulps), so it never rejects a sphere the exact candidate() would accept; NaN or inf operands
+// make the test false (keep the sphere).  Proof: Z = (t_min*a - margins) - h - 2^-30|h|;
 // Z > 0 and Z*Z > disc*(1 + 2^-30) give s < Z, hence h + s < t_min*a by more than the rounding of
-// fl(h + s), so fl(h + s) / a < t_min and root1 <= root2 <= t_min.  The filters need a within
-// [2^-400, 2^400] (else they never reject).  Typical catch: the sphere a secondary ray starts on
+// fl(h + s), so fl(h + s) / a < t_min and root1 <= root2 <= t_min.  The filter needs a within
+// [2^-400, 2^400] (else it never rejects).  Typical catch: the sphere a secondary ray starts on
 // (c ~ 0, h < 0), whose candidate otherwise costs a sqrt and two divisions for the whole wave.
 struct LeafFilter {
-    double a_tiny;  // a * 2^-600 (0 when the filters are off)
+    double a_tiny;  // a * 2^-600
     double tm_lim;  // t_min * a lowered by the margins
     bool on;
     __device__ __forceinline__ static LeafFilter make(double a, double t_min) {
@@ -308,12 +306,6 @@ struct LeafFilter {
         const double z = __builtin_fma(-__builtin_fabs(h), 0x1p-30, tm_lim - h);
         return on && z > 0 && __builtin_fma(z, z, -(disc * (1 + 0x1p-30))) > 0;
     }
-    __device__ __forceinline__ bool beyond(double h, double disc, double a, double closest) const {
-        const double pc = closest * a;
-        const double tc = __builtin_fma(__builtin_fabs(pc), 0x1p-30, pc) + a_tiny;
-        const double y = __builtin_fma(-__builtin_fabs(h), 0x1p-30, h - tc);
-        return on && y > 0 && __builtin_fma(y, y, -(disc * (1 + 0x1p-30))) > 0;
-    }
 };
 
 template <bool kLdsNodes>
@@ -324,6 +316,7 @@ struct BvhWalker {
     const uint32_t* __restrict__ asid;   // always-list original indices
     uint32_t n_always;
     int32_t* stack;                      // LDS, element i of this lane at stack[i * kBlockBvh]
+    float origin_bound;                  // BvhArgs::origin_bound
 
     // always-list sphere q: geometry + original index from global memory (uniform address,
     // read-only data: scalar loads; the compiler emits per-lane vector loads, since it cannot prove
@@ -374,12 +367,8 @@ struct BvhWalker {
         const double h = (r.dir.x * ocx + r.dir.y * ocy) + r.dir.z * ocz;
         const double c = ((ocx * ocx + ocy * ocy) + ocz * ocz) - s.r2;
         const double disc = h * h - a * c;
-#if RTZIG_LEAF_FILTER == 0
-        if (disc >= 0) candidate(sid, h, disc, ad, t_min, closest, best, found, pr);
-#else
         // the ground sphere is "behind" every ray that leaves it: no sqrt / second-root division
         if (disc >= 0 && !lfilt.behind(h, disc)) candidate(sid, h, disc, ad, t_min, closest, best, found, pr);
-#endif
     }
 
     // root selection of sphere.zig:35-41 for a sphere with disc >= 0, then the first-wins argmin.
@@ -448,6 +437,11 @@ struct BvhWalker {
         // overflowed plane is +-inf in ray order, and NaN arises only from a NaN origin, which
         // v_max3/v_min3 drop (the box is kept: permissive, never a wrong cull).
         const uint32_t ax = ix < 0 ? 8u : 0u, ay = 16u + (iy < 0 ? 8u : 0u), az = 32u + (iz < 0 ? 8u : 0u);
+        // lanes whose origin lies outside the box padding's origin bound (rt_bvh.cpp) cull nothing:
+        // their box tests are forced to "hit" on the scalar unit (a NaN origin fails every sphere
+        // test anyway; the max drops it)
+        const uint64_t far_mask = __ballot(__builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(ox), __builtin_fabsf(oy)),
+                                                           __builtin_fabsf(oz)) > origin_bound);
         // per-axis constants live in the low half of a register pair; pk_fma_lo broadcasts them to
         // both lanes of the packed fma (op_sel_hi), so they are not duplicated with v_mov
         f2 inv_x, inv_y, inv_z, noi_x, noi_y, noi_z;
@@ -508,7 +502,8 @@ struct BvhWalker {
                 // The three compares are taken as wave masks and combined on the scalar unit, and
                 // the selects are v_cndmask on those masks: 3 compares + 5 selects (the compiler's
                 // form of the same logic re-compared a negated mask on the VALU).
-                const uint64_t m0 = __ballot(n0 <= f0), m1 = __ballot(n1 <= f1), mf = __ballot(n0 <= n1);
+                const uint64_t m0 = __ballot(n0 <= f0) | far_mask, m1 = __ballot(n1 <= f1) | far_mask,
+                               mf = __ballot(n0 <= n1);
                 const uint64_t pick0 = m0 & (~m1 | mf);  // both: nearer; one: that one
                 const uint64_t any = m0 | m1, both = m0 & m1;
                 const int32_t near = sel_mask(ref1, ref0, pick0), far = sel_mask(ref0, ref1, pick0);
@@ -532,18 +527,12 @@ struct BvhWalker {
                     const double c = ((ocx * ocx + ocy * ocy) + ocz * ocz) - s.r2;
                     disc[u] = h[u] * h[u] - a * c;
                 }
-#if RTZIG_LEAF_FILTER == 0
-#pragma unroll
-                for (int u = 0; u < kLeafBvh; ++u) {
-                    if (disc[u] >= 0) candidate(lf->sid[u], h[u], disc[u], ad, t_min, closest, best, found, pr);
-                }
-#else
                 // Compacted candidates: a wave pays a candidate block (sqrt + division) whenever ANY
                 // of its lanes needs it, so each lane first drops the slots that provably cannot
                 // win (LeafFilter) and then feeds its viable slots through ONE block per round,
                 // nearest-looking (smallest h) first; a second round runs only for lanes with a
                 // second slot still viable after `closest` has shrunk.
-                if constexpr (kLeafBvh == 2 && RTZIG_LEAF_FILTER == 1) {
+                if constexpr (kLeafBvh == 2) {
                     // the same rounds written out for two slots, so the viability flags stay lane
                     // masks (the generic form keeps them as 0/1 VGPRs and re-compares them)
                     const bool v0 = disc[0] >= 0 && !lfilt.behind(h[0], disc[0]);
@@ -563,9 +552,6 @@ struct BvhWalker {
                 for (int u = 0; u < kLeafBvh; ++u) {
                     sid[u] = lf->sid[u];
                     v[u] = disc[u] >= 0 && !lfilt.behind(h[u], disc[u]);
-#if RTZIG_LEAF_FILTER >= 2
-                    v[u] = v[u] && !lfilt.beyond(h[u], disc[u], a, closest);
-#endif
                 }
 #pragma unroll
                 for (int rd = 0; rd < kLeafBvh; ++rd) {
@@ -588,14 +574,10 @@ struct BvhWalker {
 #pragma unroll
                         for (int u = 0; u < kLeafBvh; ++u) {
                             v[u] = v[u] && u != pb;
-#if RTZIG_LEAF_FILTER >= 2
-                            v[u] = v[u] && !lfilt.beyond(h[u], disc[u], a, closest);
-#endif
                         }
                     }
                 }
                 }
-#endif
                 pr.tests(kLeafBvh);
                 upper = (float)closest;
                 upper = upper + __builtin_fabsf(upper) * 0x1p-20f;
@@ -609,28 +591,22 @@ struct BvhWalker {
 };
 
 // ------------------------------------------------------------------------------------------------
-// The path state machine shared by every kernel variant: queue refill + one ray segment per lane
-// per iteration (rayColor's loop body, camera.zig:153-177) + per-sample color stores.
+// The path state machine shared by every kernel variant: unit refill (rt_units.h) + one ray segment
+// per lane per iteration (rayColor's loop body, camera.zig:153-177) + ring stores of finished
+// samples + the ordered finalisation of finished units.
 // `geo_orig` is the geometry in original list order (hit-record center of the winner).
 // ------------------------------------------------------------------------------------------------
 template <bool kProf, class Walker>
 __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& walk, const GeoRec* __restrict__ geo_orig,
-                                          const MatRec* __restrict__ mat_g, double* __restrict__ samples,
-                                          unsigned long long* __restrict__ queue,
+                                          const MatRec* __restrict__ mat_g, const UnitArgs& ua,
                                           unsigned long long* __restrict__ stats) {
     const uint32_t W = p.width;
-    const uint32_t P = p.n_rows * W;           // pixels per sample layer
-    const uint64_t total = (uint64_t)P * p.s_count;
     const uint32_t lane = lane_id();
-    const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x / 64);
-
-    // wave-uniform queue window [wq.cur, wq.end) and claim state
-    WorkQueue wq(total, nwaves, blockIdx.x);
-    bool drained = false;
+    UnitSched us(ua, blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64);
 
     // per-lane path state
     bool active = false;
-    uint64_t item = 0, slot = 0;  // queue position; store position [s][pixel]
+    uint32_t myslot = 0, mi = 0;  // the unit slot and item of the lane's path (its ring position)
     Rng g;
     Ray r;
     v3 att = mk(1, 1, 1);
@@ -649,80 +625,36 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
     while (true) {
         uint64_t t_top = 0;
         if constexpr (kProf) t_top = __builtin_amdgcn_s_memtime();
+        // ---- finalise a unit whose samples have all ended (rt_units.h) ---------------------------
+        const bool progressed = us.finalize_one(active, myslot, lane);
         // ---- hand new items to lanes without a path (wave-uniform control flow) ----------------
         bool fresh = false;
-        uint64_t needy = __ballot(!active);
-        while (needy != 0 && !drained) {
-            if (wq.cur >= wq.end) {
-                if (!wq.claim(queue, lane)) {
-                    drained = true;
-                    if constexpr (kProf) rt_drain = __builtin_amdgcn_s_memrealtime();
-                    break;
-                }
-            }
-            const uint64_t avail = wq.end - wq.cur;
-            const uint32_t want = (uint32_t)__popcll(needy);
-            const uint32_t take = avail < want ? (uint32_t)avail : want;
-            if (!active) {
-                const uint32_t rk = rank_in(needy);
-                if (rk < take) {
-                    item = wq.cur + rk;
-                    active = true;
-                    fresh = true;
-                }
-            }
-            wq.cur += take;
-            needy = __ballot(!active);
+        uint32_t fq = 0, fs = 0;  // pixel (launch-local) and sample of a freshly handed item
+        const bool was_drained = us.drained;
+        us.refill(active, fresh, myslot, mi, fq, fs, lane);
+        if constexpr (kProf) {
+            if (us.drained && !was_drained) rt_drain = __builtin_amdgcn_s_memrealtime();
         }
         // the lanes handed an item above start their path: seeding and getRay run once, outside
         // the claim loop, so the generator state and ray are not loop-carried through it
         if (fresh) {
-            // items per launch < 2^32 (host-side chunking): 32-bit index math
-            const uint32_t it32 = (uint32_t)item;
-            uint32_t s_local, q;
-            uint32_t row_local, i;
-            if (p.order == 0) {  // sample-major: a wave takes 64 neighbouring pixels of one row
-                s_local = fastdiv(it32, p.div_layer);
-                q = it32 - s_local * P;
-                row_local = fastdiv(q, p.div_width);
-                i = q - row_local * W;
-            } else if (p.order == 2) {
-                // sample-major over 8x8 pixel tiles: bands of 8 rows, each walked tile by tile (8
-                // columns x the band's rows, row-major inside a tile); q is the position in that order
-                s_local = fastdiv(it32, p.div_layer);
-                q = it32 - s_local * P;
-                const uint32_t band = fastdiv(q, p.div_width) >> 3;
-                const uint32_t rq = q - band * 8 * W;
-                const uint32_t hb = p.n_rows - band * 8 < 8 ? p.n_rows - band * 8 : 8;
-                uint32_t c, o, orow, wc;
-                if (hb == 8 && (rq >> 6) * 8 + 8 <= W) {  // a full tile: shifts
-                    c = rq >> 6;
-                    o = rq & 63;
-                    orow = o >> 3;
-                    wc = 8;
-                } else {  // the last band (n_rows % 8) or the last tile column (W % 8)
-                    c = rq / (8 * hb);
-                    o = rq - c * 8 * hb;
-                    wc = W - c * 8 < 8 ? W - c * 8 : 8;
-                    orow = o / wc;
-                }
-                i = c * 8 + (o - orow * wc);
-                row_local = band * 8 + orow;
-            } else {  // pixel-major: a wave takes consecutive samples of one pixel
-                q = it32 / p.s_count;
-                s_local = it32 - q * p.s_count;
-                row_local = fastdiv(q, p.div_width);
-                i = q - row_local * W;
-            }
-            slot = (uint64_t)s_local * P + (row_local * W + i);
+            const uint32_t row_local = fastdiv(fq, p.div_width);
+            const uint32_t i = fq - row_local * W;
             const uint32_t j = p.row0 + row_local * p.row_step;
             const uint64_t pixel = (uint64_t)j * W + i;
-            g.seed(sample_key(p.seed_mix, pixel, p.s_begin + s_local));
+            g.seed(sample_key(p.seed_mix, pixel, fs));
             dpend = camera_start(i, j, g, r);
             att = mk(1, 1, 1);
             bounce = 0;
         }
-        if (__ballot(active) == 0) break;
+        if (__ballot(active) == 0) {
+            // nothing to trace: finish, or claim again next iteration, or wait for the previous chunk
+            // of a tile another wave holds
+            if (us.busy == 0 && us.drained) break;
+            if (!progressed && !us.can_claim() && !us.wait(lane)) break;
+            // else: the rest of the iteration runs with every lane idle (no back edge of its own:
+            // one measured 17 extra VGPRs)
+        }
         uint64_t t_walk0 = 0, t_walk1 = 0;
         if constexpr (kProf) {
             t_walk0 = __builtin_amdgcn_s_memtime();
@@ -746,11 +678,6 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
             const bool wr = pending && !got, wd = dpend && !dgot;
             const uint64_t need = __ballot(wr || wd);
             if (need == 0) break;
-#if RTZIG_TRIP_DEFER > 0
-            // a late trip that only a few lanes need is left to the next iteration (those lanes stay
-            // pending and skip one walk) instead of costing the whole wave a trip now
-            if (trip > 0 && __popcll(need) <= RTZIG_TRIP_DEFER) break;
-#endif
             if (wr || wd) {
                 ux = g.range_pm1();
                 uy = g.range_pm1();
@@ -874,10 +801,7 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
             }
         }
         if (done) {
-            double* dst = samples + 3 * slot;
-            dst[0] = col.x;
-            dst[1] = col.y;
-            dst[2] = col.z;
+            us.store(myslot, mi, col.x, col.y, col.z);
             ++nsamples;
             active = false;
         }
@@ -956,8 +880,8 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
 // Linear-walk kernel: geometry in LDS (kLds) or read by scalar loads from global memory.
 template <bool kLds, int U, int kWaves, bool kProf>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kWaves))) void sample_kernel(
-    KernelParams p, const GeoRec* __restrict__ geo_g, const MatRec* __restrict__ mat_g,
-    double* __restrict__ samples, unsigned long long* __restrict__ queue, unsigned long long* __restrict__ stats) {
+    KernelParams p, const GeoRec* __restrict__ geo_g, const MatRec* __restrict__ mat_g, UnitArgs ua,
+    unsigned long long* __restrict__ stats) {
     extern __shared__ GeoRec lds_geo[];
     const GeoRec* geo = geo_g;
     if constexpr (kLds) {
@@ -965,7 +889,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kWaves))
         __syncthreads();
         geo = lds_geo;
     }
-    path_loop<kProf>(p, LinearWalker<U>{geo, p.n_pad, p.n_spheres}, geo, mat_g, samples, queue, stats);
+    path_loop<kProf>(p, LinearWalker<U>{geo, p.n_pad, p.n_spheres}, geo, mat_g, ua, stats);
 }
 
 // BVH-walk kernel: nodes + slot geometry + slot ids staged in LDS (kLdsScene) or read from global
@@ -973,9 +897,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kWaves))
 template <bool kLdsScene, bool kProf>
 __global__ __launch_bounds__(kBlockBvh) void sample_kernel_bvh(KernelParams p, BvhArgs b,
                                                                const GeoRec* __restrict__ geo_g,
-                                                               const MatRec* __restrict__ mat_g,
-                                                               double* __restrict__ samples,
-                                                               unsigned long long* __restrict__ queue,
+                                                               const MatRec* __restrict__ mat_g, UnitArgs ua,
                                                                unsigned long long* __restrict__ stats) {
     // LDS: [nodes][leaves] (kLdsScene) at address 0, so a node's byte-offset ref IS its LDS
     // address; then the per-lane stacks [kMaxDepthBvh][kBlockBvh]
@@ -995,112 +917,9 @@ __global__ __launch_bounds__(kBlockBvh) void sample_kernel_bvh(KernelParams p, B
         nodes = ln;
         leaves = ll;
     }
-    path_loop<kProf>(p, BvhWalker<kLdsScene>{nodes, leaves, b.always_geo, b.always_sid, b.n_always, stack + threadIdx.x}, geo_g,
-                     mat_g, samples, queue, stats);
-}
-
-#ifndef RTZIG_REDUCE_COAL
-#define RTZIG_REDUCE_COAL 0
-#endif
-#ifndef RTZIG_REDUCE_NT
-#define RTZIG_REDUCE_NT 0
-#endif
-template <int kOut>
-__global__ __launch_bounds__(256) void reduce_kernel(ReduceParams p, const double* __restrict__ samples,
-                                                     double* __restrict__ sums, void* __restrict__ out) {
-#if RTZIG_REDUCE_COAL
-    // element-wise: thread t of block b sums the elements e = 768 b + t + 256 k (k = 0..2) of every
-    // [pixel][channel] sample layer.  Each channel's sum is independent and runs in sample order,
-    // so the additions are those of the per-pixel form; every load and store of a wave is one
-    // contiguous 512-B run instead of three 24-B-strided ones.
-    {
-        const uint64_t n_el = 3 * (uint64_t)p.n_pixels;
-        const uint64_t e0 = 768 * (uint64_t)blockIdx.x + threadIdx.x;
-        const bool v0 = e0 < n_el, v1 = e0 + 256 < n_el, v2 = e0 + 512 < n_el;
-        double a0 = 0.0, a1 = 0.0, a2 = 0.0;
-        if (!p.first) {
-            if (v0) a0 = sums[e0];
-            if (v1) a1 = sums[e0 + 256];
-            if (v2) a2 = sums[e0 + 512];
-        }
-        const double* src = samples + e0;
-        if (v2) {
-#pragma unroll 8
-            for (uint32_t s = 0; s < p.s_count; ++s) {
-                a0 = a0 + src[0];
-                a1 = a1 + src[256];
-                a2 = a2 + src[512];
-                src += n_el;
-            }
-        } else {  // the last block
-            for (uint32_t s = 0; s < p.s_count; ++s) {
-                if (v0) a0 = a0 + src[0];
-                if (v1) a1 = a1 + src[256];
-                src += n_el;
-            }
-        }
-        const double a[3] = {a0, a1, a2};
-        const bool v[3] = {v0, v1, v2};
-#pragma unroll
-        for (int k = 0; k < 3; ++k) {
-            if (!v[k]) continue;
-            const uint64_t e = e0 + 256 * k;
-            if (!p.last) {
-                sums[e] = a[k];
-            } else if constexpr (kOut == 0) {
-                ((double*)out)[e] = a[k] * p.scale;  // avgColor = pixelColor * pixelSamplesScale
-            } else {
-                ((uint8_t*)out)[e] = to_byte(a[k] * p.scale);
-            }
-        }
-        return;
-    }
-#endif
-    const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
-    if (q >= p.n_pixels) return;
-    double x = 0.0, y = 0.0, z = 0.0;
-    if (!p.first) {
-        x = sums[3 * (uint64_t)q + 0];
-        y = sums[3 * (uint64_t)q + 1];
-        z = sums[3 * (uint64_t)q + 2];
-    }
-    const double* src = samples + 3 * (uint64_t)q;
-    const uint64_t stride = 3 * (uint64_t)p.n_pixels;
-#pragma unroll 8
-    for (uint32_t s = 0; s < p.s_count; ++s) {
-#if RTZIG_REDUCE_NT
-        // streamed once: non-temporal loads (no reuse to keep in L2 / MALL)
-        x = x + __builtin_nontemporal_load(src + 0);
-        y = y + __builtin_nontemporal_load(src + 1);
-        z = z + __builtin_nontemporal_load(src + 2);
-#else
-        x = x + src[0];
-        y = y + src[1];
-        z = z + src[2];
-#endif
-        src += stride;
-    }
-    if (!p.last) {
-        sums[3 * (uint64_t)q + 0] = x;
-        sums[3 * (uint64_t)q + 1] = y;
-        sums[3 * (uint64_t)q + 2] = z;
-        return;
-    }
-    // avgColor = pixelColor * pixelSamplesScale (camera.zig:137)
-    x = x * p.scale;
-    y = y * p.scale;
-    z = z * p.scale;
-    if constexpr (kOut == 0) {
-        double* dst = (double*)out + 3 * (uint64_t)q;
-        dst[0] = x;
-        dst[1] = y;
-        dst[2] = z;
-    } else {
-        uint8_t* dst = (uint8_t*)out + 3 * (uint64_t)q;
-        dst[0] = to_byte(x);
-        dst[1] = to_byte(y);
-        dst[2] = to_byte(z);
-    }
+    path_loop<kProf>(p, BvhWalker<kLdsScene>{nodes, leaves, b.always_geo, b.always_sid, b.n_always, stack + threadIdx.x,
+                                              b.origin_bound}, geo_g,
+                     mat_g, ua, stats);
 }
 
 }  // namespace rtk
@@ -1154,13 +973,19 @@ uint32_t persistent_blocks(K kernel, size_t shmem) {
     return b;
 }
 
+// blocks of a persistent launch: resident capacity, the work, and the ring's wave capacity
+uint32_t grid_blocks(uint64_t need, uint64_t cap, const rtk::UnitArgs* ua, uint32_t block) {
+    const uint64_t ring_blocks = ua->ring_waves / (block / 64);
+    uint64_t b = need < cap ? need : cap;
+    return (uint32_t)(b < ring_blocks ? b : ring_blocks);
+}
+
 template <bool kLds, int U, int kWaves>
-void launch_samples(const rtk::KernelParams* p, const rtk::GeoRec* geo, const rtk::MatRec* mat, double* samples,
-                    unsigned long long* qu, unsigned long long* st, hipStream_t stream, size_t shmem, uint64_t need) {
+void launch_samples(const rtk::KernelParams* p, const rtk::GeoRec* geo, const rtk::MatRec* mat,
+                    const rtk::UnitArgs* ua, unsigned long long* st, hipStream_t stream, size_t shmem, uint64_t need) {
     auto kernel = p->prof ? rtk::sample_kernel<kLds, U, kWaves, true> : rtk::sample_kernel<kLds, U, kWaves, false>;
-    const uint32_t cap = persistent_blocks(kernel, shmem);
-    const uint32_t blocks = (uint32_t)(need < cap ? need : cap);
-    hipLaunchKernelGGL(kernel, dim3(blocks), dim3(rtk::kBlock), shmem, stream, *p, geo, mat, samples, qu, st);
+    const uint32_t blocks = grid_blocks(need, persistent_blocks(kernel, shmem), ua, rtk::kBlock);
+    hipLaunchKernelGGL(kernel, dim3(blocks), dim3(rtk::kBlock), shmem, stream, *p, geo, mat, *ua, st);
 }
 
 // Kernel variant: RTZIG_KERNEL=<geom>_u<U>[_w<waves>], geom in {lds, smem}; default kDefaultVariant.
@@ -1172,10 +997,7 @@ struct Variant {
     int unroll;
     int waves;
 };
-constexpr Variant kVariants[] = {
-    {"lds_u1", true, 1, 1},  {"lds_u2", true, 2, 1},  {"lds_u4", true, 4, 1},  {"lds_u4_w5", true, 4, 5},
-    {"smem_u1", false, 1, 1}, {"smem_u2", false, 2, 1}, {"smem_u4", false, 4, 1}, {"smem_u4_w5", false, 4, 5},
-};
+constexpr Variant kVariants[] = {{"lds_u4", true, 4, 1}, {"smem_u4", false, 4, 1}};
 
 const Variant& variant_choice(bool fits_lds) {
     const char* e = std::getenv("RTZIG_KERNEL");
@@ -1184,13 +1006,13 @@ const Variant& variant_choice(bool fits_lds) {
         if (std::strcmp(v.name, want) == 0 && (fits_lds || !v.lds)) return v;
     for (const Variant& v : kVariants)
         if (std::strcmp(v.name, rtk::kDefaultVariant) == 0 && (fits_lds || !v.lds)) return v;
-    return kVariants[6];  // smem_u4: works for any sphere count
+    return kVariants[1];  // smem_u4: works for any sphere count
 }
 
 }  // namespace
 
 extern "C" hipError_t rtk_launch_samples(const rtk::KernelParams* p, const rtk::GeoRec* geo,
-                                         const rtk::MatRec* mat, double* samples, void* queue,
+                                         const rtk::MatRec* mat, const rtk::UnitArgs* ua,
                                          void* stats, hipStream_t stream, const char** name) {
     using namespace rtk;
     const uint64_t total = (uint64_t)p->n_rows * p->width * p->s_count;
@@ -1199,24 +1021,20 @@ extern "C" hipError_t rtk_launch_samples(const rtk::KernelParams* p, const rtk::
     const size_t shmem = v.lds ? (size_t)p->n_pad * sizeof(GeoRec) : 0;
     const uint64_t need = (total + kBlock - 1) / kBlock;
     auto* st = (unsigned long long*)stats;
-    auto* qu = (unsigned long long*)queue;
-    hipError_t e = hipMemsetAsync(queue, 0, kQueueBytes, stream);
-    if (e != hipSuccess) return e;
     if (name) *name = v.name;
 #define RTK_CASE(L, U, W)                                                                 \
     if (v.lds == L && v.unroll == U && v.waves == W) {                                   \
-        launch_samples<L, U, W>(p, geo, mat, samples, qu, st, stream, shmem, need);      \
+        launch_samples<L, U, W>(p, geo, mat, ua, st, stream, shmem, need);               \
         return hipGetLastError();                                                        \
     }
-    RTK_CASE(true, 1, 1) RTK_CASE(true, 2, 1) RTK_CASE(true, 4, 1) RTK_CASE(true, 4, 5)
-    RTK_CASE(false, 1, 1) RTK_CASE(false, 2, 1) RTK_CASE(false, 4, 1) RTK_CASE(false, 4, 5)
+    RTK_CASE(true, 4, 1) RTK_CASE(false, 4, 1)
 #undef RTK_CASE
     return hipErrorInvalidValue;
 }
 
 extern "C" hipError_t rtk_launch_samples_bvh(const rtk::KernelParams* p, const rtk::BvhArgs* b,
-                                             const rtk::GeoRec* geo, const rtk::MatRec* mat, double* samples,
-                                             void* queue, void* stats, hipStream_t stream, const char** name) {
+                                             const rtk::GeoRec* geo, const rtk::MatRec* mat, const rtk::UnitArgs* ua,
+                                             void* stats, hipStream_t stream, const char** name) {
     using namespace rtk;
     const uint64_t total = (uint64_t)p->n_rows * p->width * p->s_count;
     if (total == 0) return hipSuccess;
@@ -1227,34 +1045,18 @@ extern "C" hipError_t rtk_launch_samples_bvh(const rtk::KernelParams* p, const r
     const bool lds_scene = stack_bytes + scene_bytes <= 80 * 1024;
     const size_t shmem = stack_bytes + (lds_scene ? scene_bytes : 0);
     const uint64_t need = (total + kBlockBvh - 1) / kBlockBvh;
-    hipError_t e = hipMemsetAsync(queue, 0, kQueueBytes, stream);
-    if (e != hipSuccess) return e;
     auto* st = (unsigned long long*)stats;
-    auto* qu = (unsigned long long*)queue;
     auto launch = [&](auto kernel, const char* nm) -> hipError_t {
         uint32_t cap32 = 0;
         const hipError_t ea = rtk_resident_blocks((const void*)kernel, kBlockBvh, shmem, &cap32);
         if (ea != hipSuccess) return ea;
-        const uint64_t cap = cap32;
-        const uint32_t blocks = (uint32_t)(need < cap ? need : cap);
+        const uint32_t blocks = grid_blocks(need, cap32, ua, kBlockBvh);
         if (name) *name = nm;
-        hipLaunchKernelGGL(kernel, dim3(blocks), dim3(kBlockBvh), shmem, stream, *p, *b, geo, mat, samples, qu, st);
+        hipLaunchKernelGGL(kernel, dim3(blocks), dim3(kBlockBvh), shmem, stream, *p, *b, geo, mat, *ua, st);
         return hipGetLastError();
     };
     if (p->prof)
         return lds_scene ? launch(sample_kernel_bvh<true, true>, "bvh_lds(prof)")
                          : launch(sample_kernel_bvh<false, true>, "bvh_global(prof)");
     return lds_scene ? launch(sample_kernel_bvh<true, false>, "bvh_lds") : launch(sample_kernel_bvh<false, false>, "bvh_global");
-}
-
-extern "C" hipError_t rtk_launch_reduce(const rtk::ReduceParams* p, const double* samples, double* sums,
-                                        void* out, hipStream_t stream) {
-    using namespace rtk;
-    if (p->n_pixels == 0) return hipSuccess;
-    const uint32_t blocks = (p->n_pixels + 255) / 256;
-    if (p->out_format == 0)
-        hipLaunchKernelGGL((reduce_kernel<0>), dim3(blocks), dim3(256), 0, stream, *p, samples, sums, out);
-    else
-        hipLaunchKernelGGL((reduce_kernel<1>), dim3(blocks), dim3(256), 0, stream, *p, samples, sums, out);
-    return hipGetLastError();
 }

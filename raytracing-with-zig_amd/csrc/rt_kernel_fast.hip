@@ -22,6 +22,7 @@
 
 #include "rt_device.h"
 #include "rt_kernel.h"
+#include "rt_units.h"
 
 #pragma clang fp contract(fast)
 
@@ -33,8 +34,8 @@ using rtk::BvhNode;
 using rtk::GeoRec;
 using rtk::KernelParams;
 using rtk::kBlockBvh;
-using rtk::kChunk;
-using rtk::WorkQueue;
+using rtk::UnitArgs;
+using rtk::UnitSched;
 using rtk::kLeafBvh;
 using rtk::MatRec;
 using rtk::Rng;
@@ -171,6 +172,7 @@ struct Walker {
     const uint32_t* __restrict__ asid;
     uint32_t n_always;
     int32_t* stack;
+    float origin_bound;
 
     __device__ __forceinline__ int operator()(const Ray& r, float t_min, float t_max, float* t_hit) const {
         int best = -1;
@@ -225,6 +227,9 @@ struct Walker {
         if (__builtin_fabsf(dz) < 1e-30f) dz = __builtin_copysignf(1e-30f, dz);
         const float ix = __builtin_amdgcn_rcpf(dx), iy = __builtin_amdgcn_rcpf(dy), iz = __builtin_amdgcn_rcpf(dz);
         const uint32_t ax = ix < 0 ? 8u : 0u, ay = 16u + (iy < 0 ? 8u : 0u), az = 32u + (iz < 0 ? 8u : 0u);
+        // origins outside the boxes' origin bound cull nothing (see rtk::BvhArgs::origin_bound)
+        const bool far = __builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(r.orig.x), __builtin_fabsf(r.orig.y)),
+                                         __builtin_fabsf(r.orig.z)) > origin_bound;
         const f2 inv_x = {ix, ix}, inv_y = {iy, iy}, inv_z = {iz, iz};
         const f2 noi_x = {-(r.orig.x * ix), -(r.orig.x * ix)}, noi_y = {-(r.orig.y * iy), -(r.orig.y * iy)},
                  noi_z = {-(r.orig.z * iz), -(r.orig.z * iz)};
@@ -266,8 +271,8 @@ struct Walker {
                 const f2 tz1 = __builtin_elementwise_fma(bz1, inv_z, noi_z);
                 const float n0 = slab_near(tx0.x, ty0.x, tz0.x, lower), f0 = slab_far(tx0.y, ty0.y, tz0.y, upper);
                 const float n1 = slab_near(tx1.x, ty1.x, tz1.x, lower), f1 = slab_far(tx1.y, ty1.y, tz1.y, upper);
-                const bool h0 = n0 <= f0;
-                const bool h1 = n1 <= f1;
+                const bool h0 = n0 <= f0 || far;
+                const bool h1 = n1 <= f1 || far;
                 const bool first0 = n0 <= n1;
                 top[kBlockBvh] = first0 ? ref1 : ref0;
                 const bool pick0 = h0 && (!h1 || first0);
@@ -305,20 +310,15 @@ struct Walker {
 
 template <class Walker>
 __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& walk, const GeoRec* __restrict__ geo_orig,
-                                          const MatRec* __restrict__ mat_g, double* __restrict__ samples,
-                                          unsigned long long* __restrict__ queue,
+                                          const MatRec* __restrict__ mat_g, const UnitArgs& ua,
                                           unsigned long long* __restrict__ stats) {
     const uint32_t W = p.width;
-    const uint32_t P = p.n_rows * W;
-    const uint64_t total = (uint64_t)P * p.s_count;
     const uint32_t lane = lane_id();
-    const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x / 64);
     const float t_min = (float)p.t_min, t_max = (float)p.t_max;
 
-    WorkQueue wq(total, nwaves, blockIdx.x);  // segmented queue (rt_kernel.h), as the parity kernel
-    bool drained = false;
+    UnitSched us(ua, blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64);  // as the parity kernel
     bool active = false, pending = false, sc_metal = false, dpend = false;
-    uint64_t item = 0, slot = 0;
+    uint32_t myslot = 0, mi = 0;
     Rng g;
     Ray r;
     f3 att = mk(1, 1, 1), sc_nrm = mk(0, 0, 0), sc_refl = mk(0, 0, 0);
@@ -327,50 +327,28 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
     uint64_t rays = 0, nsamples = 0;
 
     while (true) {
+        const bool progressed = us.finalize_one(active, myslot, lane);
         // ---- refill (as the parity kernel's path_loop) -----------------------------------------
         bool fresh = false;
-        uint64_t needy = __ballot(!active);
-        while (needy != 0 && !drained) {
-            if (wq.cur >= wq.end && !wq.claim(queue, lane)) {
-                drained = true;
-                break;
-            }
-            const uint64_t avail = wq.end - wq.cur;
-            const uint32_t want = (uint32_t)__popcll(needy);
-            const uint32_t take = avail < want ? (uint32_t)avail : want;
-            if (!active) {
-                const uint32_t rk = rank_in(needy);
-                if (rk < take) {
-                    item = wq.cur + rk;
-                    active = true;
-                    fresh = true;
-                }
-            }
-            wq.cur += take;
-            needy = __ballot(!active);
-        }
+        uint32_t fq = 0, fs = 0;
+        us.refill(active, fresh, myslot, mi, fq, fs, lane);
         // the lanes handed an item above start their path: seeding and getRay run once, outside
         // the claim loop, so the generator state and ray are not loop-carried through it
         if (fresh) {
-            const uint32_t it32 = (uint32_t)item;
-            uint32_t s_local, q;
-            if (p.order == 0) {  // sample-major: a wave takes 64 neighbouring pixels
-                s_local = rtk::fastdiv(it32, p.div_layer);
-                q = it32 - s_local * P;
-            } else {
-                q = it32 / p.s_count;
-                s_local = it32 - q * p.s_count;
-            }
-            slot = (uint64_t)s_local * P + q;
-            const uint32_t row_local = rtk::fastdiv(q, p.div_width);
-            const uint32_t i = q - row_local * W;
+            const uint32_t row_local = rtk::fastdiv(fq, p.div_width);
+            const uint32_t i = fq - row_local * W;
             const uint32_t j = p.row0 + row_local * p.row_step;
-            g.seed(rtk::sample_key(p.seed_mix, (uint64_t)j * W + i, p.s_begin + s_local));
+            g.seed(rtk::sample_key(p.seed_mix, (uint64_t)j * W + i, fs));
             dpend = camera_start(i, j, g, r);
             att = mk(1, 1, 1);
             bounce = 0;
         }
-        if (__ballot(active) == 0) break;
+        if (__ballot(active) == 0) {
+            if (us.busy == 0 && us.drained) break;
+            if (!progressed && !us.can_claim() && !us.wait(lane)) break;
+            // else: the rest of the iteration runs with every lane idle (no back edge of its own:
+            // one measured 17 extra VGPRs)
+        }
 
         // ---- one capped loop for randomUnitVec and randomInUnitDisk trips ----------------------
         bool done = false;
@@ -469,10 +447,7 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
             }
         }
         if (done) {
-            double* dst = samples + 3 * slot;
-            dst[0] = col.x;
-            dst[1] = col.y;
-            dst[2] = col.z;
+            us.store(myslot, mi, col.x, col.y, col.z);
             ++nsamples;
             active = false;
         }
@@ -492,9 +467,7 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
 template <bool kLdsScene>
 __global__ __launch_bounds__(kBlockBvh) void sample_kernel_fast(KernelParams p, BvhArgs b,
                                                                 const GeoRec* __restrict__ geo_g,
-                                                                const MatRec* __restrict__ mat_g,
-                                                                double* __restrict__ samples,
-                                                                unsigned long long* __restrict__ queue,
+                                                                const MatRec* __restrict__ mat_g, UnitArgs ua,
                                                                 unsigned long long* __restrict__ stats) {
     extern __shared__ __align__(16) unsigned char lds_raw[];
     const size_t scene_bytes =
@@ -512,15 +485,15 @@ __global__ __launch_bounds__(kBlockBvh) void sample_kernel_fast(KernelParams p, 
         nodes = ln;
         leaves = ll;
     }
-    path_loop(p, Walker<kLdsScene>{nodes, leaves, b.always_geo, b.always_sid, b.n_always, stack + threadIdx.x}, geo_g,
-              mat_g, samples, queue, stats);
+    path_loop(p, Walker<kLdsScene>{nodes, leaves, b.always_geo, b.always_sid, b.n_always, stack + threadIdx.x, b.origin_bound},
+              geo_g, mat_g, ua, stats);
 }
 
 }  // namespace rtf
 
 extern "C" hipError_t rtk_launch_samples_fast(const rtk::KernelParams* p, const rtk::BvhArgs* b,
-                                              const rtk::GeoRec* geo, const rtk::MatRec* mat, double* samples,
-                                              void* queue, void* stats, hipStream_t stream, const char** name) {
+                                              const rtk::GeoRec* geo, const rtk::MatRec* mat, const rtk::UnitArgs* ua,
+                                              void* stats, hipStream_t stream, const char** name) {
     using namespace rtk;
     const uint64_t total = (uint64_t)p->n_rows * p->width * p->s_count;
     if (total == 0) return hipSuccess;
@@ -530,17 +503,16 @@ extern "C" hipError_t rtk_launch_samples_fast(const rtk::KernelParams* p, const 
     const bool lds_scene = stack_bytes + scene_bytes <= 80 * 1024;
     const size_t shmem = stack_bytes + (lds_scene ? scene_bytes : 0);
     const uint64_t need = (total + kBlockBvh - 1) / kBlockBvh;
-    hipError_t e = hipMemsetAsync(queue, 0, kQueueBytes, stream);
-    if (e != hipSuccess) return e;
     auto launch = [&](auto kernel, const char* nm) -> hipError_t {
         uint32_t cap32 = 0;
         const hipError_t ea = rtk_resident_blocks((const void*)kernel, kBlockBvh, shmem, &cap32);
         if (ea != hipSuccess) return ea;
-        const uint64_t cap = cap32;
-        const uint32_t blocks = (uint32_t)(need < cap ? need : cap);
+        uint64_t blocks = need < cap32 ? need : cap32;
+        const uint64_t ring_blocks = ua->ring_waves / (kBlockBvh / 64);
+        if (blocks > ring_blocks) blocks = ring_blocks;
         if (name) *name = nm;
-        hipLaunchKernelGGL(kernel, dim3(blocks), dim3(kBlockBvh), shmem, stream, *p, *b, geo, mat, samples,
-                           (unsigned long long*)queue, (unsigned long long*)stats);
+        hipLaunchKernelGGL(kernel, dim3((uint32_t)blocks), dim3(kBlockBvh), shmem, stream, *p, *b, geo, mat, *ua,
+                           (unsigned long long*)stats);
         return hipGetLastError();
     };
     return lds_scene ? launch(rtf::sample_kernel_fast<true>, "fast_f32_lds") : launch(rtf::sample_kernel_fast<false>, "fast_f32_global");

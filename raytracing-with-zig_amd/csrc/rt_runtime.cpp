@@ -1,19 +1,30 @@
 // rt_runtime.cpp — device runtime behind the C ABI: contexts, scene upload, launches, and the
 // blocking multi-GPU rt_render() that replaces Camera.render (camera.zig:123-145).
 //
-// Multi-GPU inside one call: one host thread drives every device asynchronously (one stream per
-// GPU).  Rows are interleaved (row j on device j mod G) so sky-heavy and ground-heavy rows spread
-// evenly; each device renders its rows into its own buffer, copies them back, and the host
-// un-interleaves them into the caller's framebuffer.  Because the RNG is keyed by the GLOBAL pixel
-// index, the image is bit-identical for any device count.
+// One render of rows = ONE persistent launch of the sample kernel.  It accumulates every pixel's
+// samples in sample order itself (rt_kernel.h "Work units", rt_units.h): work units of 64 pixels x
+// a chunk of samples, wave-private rings for the colors of unfinished units, and per-pixel running
+// sums handed from wave to wave behind a per-tile flag.  The workspace is fixed: the rings (96 KiB
+// per resident wave, ≈ 0.8 GB on 256 CUs) plus 24 B of running sum per pixel and 4 B of flag per
+// 64 pixels — independent of spp, and no reduce pass.
+//
+// rt_render() keeps one cached context per device for the life of the process (SURVEY §8(b):
+// "an optional rt_context handle caches device init"): the first call creates them on parallel
+// host threads; a later call on the same sphere list uploads nothing and rebuilds nothing.
+// Multi-GPU inside one call: rows are interleaved (row j on device j mod G), each device renders its
+// rows into its own buffer, copies them to pinned host memory, and the host un-interleaves them into
+// the caller's framebuffer.  The RNG is keyed by the GLOBAL pixel index, so the image is
+// bit-identical for any device count.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
-#include <cstdlib>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <limits>
+#include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/rt.h"
@@ -23,47 +34,75 @@
 
 void rt_set_last_error(const std::string& msg);
 
+namespace {
+
+constexpr uint32_t kMaxTimed = 1024;  // event-pool bound of rt_context_kernel_times_total
+constexpr uint32_t kMaxWavesPerCU = 32;  // gfx950: 4 SIMDs x 8 wave slots (the ring's capacity)
+
+// Host-side scene: device records of the Hittable list plus its BVH, built once per sphere list and
+// uploaded to every device that renders it.
+struct SceneData {
+    std::vector<rt_sphere> spheres;
+    std::vector<rtk::GeoRec> geo;  // padded to kPad with never-hit sentinels
+    std::vector<rtk::MatRec> mat;
+    bool bvh_ok = false;
+    double origin_bound = 0;
+    std::vector<rtk::BvhNode> nodes;
+    std::vector<rtk::BvhLeaf> leaves;
+    std::vector<rtk::GeoRec> ageo;
+    std::vector<uint32_t> asid;
+    uint32_t n_nodes = 0, n_leaves = 0, n_always = 0, depth = 0;
+};
+
+}  // namespace
+
 struct rt_context {
     int device = 0;
-    hipStream_t stream = nullptr;
+    hipStream_t stream = nullptr;   // uploads, and the stream rt_render renders on
     rtk::GeoRec* d_geo = nullptr;
     rtk::MatRec* d_mat = nullptr;
     uint32_t n_spheres = 0;
     uint32_t capacity = 0;
-    // workspace: per-sample colors [s][pixel][3] (HBM is 288 GB: a whole 1200x800x500 frame of
-    // samples is 11.5 GB), running per-pixel sums for multi-chunk renders, the work-queue counter
-    double* d_samples = nullptr;
-    size_t samples_bytes = 0;
+    // workspace (rt_kernel.h "Work units"): wave rings, running sums, per-tile flags, counters
+    double* d_ring = nullptr;
+    size_t ring_bytes = 0;
+    uint32_t ring_waves = 0;
     double* d_sums = nullptr;
     size_t sums_bytes = 0;
-    unsigned long long* d_queue = nullptr;
+    uint32_t* d_flags = nullptr;
+    size_t flags_bytes = 0;
+    unsigned long long* d_ctr = nullptr;  // rtk::kCtrBytes, zeroed per launch ([8]: error word)
     const char* last_kernel = "sample_kernel";
-    // BVH over the sphere list (rt_bvh.hpp); empty/!ok => the linear walk
-    std::vector<rt_sphere> spheres;  // host copy (rebuilds for far-away cameras)
-    bool bvh_ok = false;
-    double bvh_origin_bound = 0;
+    SceneData scene;                // host copy (BVH rebuilds for far-away cameras, scene comparisons)
+    rtk::BvhArgs bvh{};
     rtk::BvhNode* d_nodes = nullptr;
     rtk::BvhLeaf* d_leaves = nullptr;
     rtk::GeoRec* d_always_geo = nullptr;
     uint32_t* d_always_sid = nullptr;
     size_t nodes_bytes = 0, leaves_bytes = 0, always_geo_bytes = 0, always_sid_bytes = 0;
-    rtk::BvhArgs bvh{};
-    // optional per-kernel timing: event pairs around every sample / reduce launch of the last call
+    // ordering: `done` is recorded on the caller's stream after the launch of a render call; device
+    // buffers are only rewritten after it (quiesce), and a render on another stream first waits for it
+    hipEvent_t done = nullptr;
+    bool done_valid = false;
+    hipStream_t done_stream = nullptr;
+    // optional kernel timing: an event pair around every launch
     bool timing = false;
     bool profile = false;  // instrumented kernels: d_stats must hold 24 uint64 (rt.h)
     int precision = RT_PRECISION_F64;
-    // event pool: every timed chunk of every call takes the next 4 events (sample start/stop,
-    // reduce start/stop); `call_first` / `timed_chunks` locate the last call's, `log_used` counts
-    // the chunks recorded since timing was (re)enabled (rt_context_kernel_times_total)
-    std::vector<hipEvent_t> events;
+    std::vector<hipEvent_t> events;  // 2 per timed launch: start, stop
     uint32_t call_first = 0;
-    uint32_t timed_chunks = 0;
+    uint32_t timed_calls = 0;
     uint32_t log_used = 0;
+    // rt_render's cached output staging (device rows + pinned host copy + stats)
+    void* d_out = nullptr;
+    size_t d_out_bytes = 0;
+    void* h_out = nullptr;
+    size_t h_out_bytes = 0;
+    uint64_t* d_stats = nullptr;
+    uint64_t* h_stats = nullptr;
 };
 
 namespace {
-
-constexpr uint32_t kMaxTimedChunks = 1024;  // event-pool bound of rt_context_kernel_times_total
 
 int hip_fail(hipError_t e, const char* what) {
     rt_set_last_error(std::string(what) + ": " + hipGetErrorString(e));
@@ -109,69 +148,45 @@ int validate_spheres(const rt_sphere* s, size_t n) {
     return RT_OK;
 }
 
-// Workspace budget for per-sample colors: RTZIG_WORKSPACE_MB, default 64 GiB (MI355X has 288 GB
-// of HBM; a whole config-4 frame needs 11.5 GB), never more than 60% of the free memory.
-uint64_t workspace_budget() {
-    uint64_t budget = 64ULL << 30;
-    if (const char* e = std::getenv("RTZIG_WORKSPACE_MB")) budget = std::strtoull(e, nullptr, 10) << 20;
-    size_t free_b = 0, total_b = 0;
-    if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b > 0) {
-        const uint64_t cap = (uint64_t)(0.6 * (double)free_b);
-        if (budget > cap) budget = cap;
-    }
-    return budget;
-}
-
-int ensure_buffer(void** ptr, size_t* bytes, size_t need) {
-    if (*ptr && *bytes >= need) return RT_OK;
-    (void)hipFree(*ptr);
-    *ptr = nullptr;
-    *bytes = 0;
-    hipError_t e = hipMalloc(ptr, need ? need : 1);
-    if (e != hipSuccess) return hip_fail(e, "hipMalloc(workspace)");
-    *bytes = need;
-    return RT_OK;
-}
-
-// Builder ref (node index >= 0, ~leaf index < 0) -> device ref (byte offsets, see upload_bvh).
+// Builder ref (node index >= 0, ~leaf index < 0) -> device ref (byte offsets, see build_bvh).
 int32_t device_ref(int32_t ref) {
     if (ref >= 0) return (int32_t)((int64_t)ref * (int64_t)sizeof(rtk::BvhNode));
     return ~(int32_t)((int64_t)(~ref) * (int64_t)sizeof(rtk::BvhLeaf));
 }
 
-// Builds and uploads the BVH for the context's scene, valid for ray origins with |o_i| <= bound.
-int upload_bvh(rt_context* ctx, double bound) {
-    const rtbvh::Bvh bvh = rtbvh::build(ctx->spheres.data(), ctx->spheres.size(), bound);
+rtk::GeoRec geo_of(const rt_sphere* s) {
+    rtk::GeoRec g;
+    if (!s) {  // never-hit sentinel (rt_kernel.h)
+        g.cx = g.cy = g.cz = 0.0;
+        g.r2 = -std::numeric_limits<double>::infinity();
+        return g;
+    }
+    const double r = s->radius > 0 ? s->radius : 0.0;  // Sphere.init clamps (sphere.zig:21)
+    g.cx = s->center[0];
+    g.cy = s->center[1];
+    g.cz = s->center[2];
+    g.r2 = r * r;
+    return g;
+}
+
+// The BVH of sd.spheres, valid for ray origins with |o_i| <= bound (device layout, rt_kernel.h).
+void build_bvh(SceneData& sd, double bound) {
+    const rtbvh::Bvh bvh = rtbvh::build(sd.spheres.data(), sd.spheres.size(), bound);
     // byte-offset refs must fit int32 (and stay clear of the walk's INT32_MIN "done" marker)
     const bool fits = bvh.nodes.size() * sizeof(rtk::BvhNode) < (1ull << 30) &&
                       bvh.slot_to_sphere.size() / rtk::kLeafBvh * sizeof(rtk::BvhLeaf) < (1ull << 30);
-    ctx->bvh_ok = bvh.ok && fits;
-    ctx->bvh_origin_bound = bound;
-    if (!ctx->bvh_ok) return RT_OK;
+    sd.bvh_ok = bvh.ok && fits;
+    sd.origin_bound = bound;
+    if (!sd.bvh_ok) return;
     static_assert(rtbvh::kLeafMax == rtk::kLeafBvh && rtbvh::kMaxDepth == rtk::kMaxDepthBvh, "BVH constants differ");
     const size_t nn = bvh.nodes.size();
     const size_t na = bvh.n_always;
     const size_t nl = (bvh.slot_to_sphere.size() - na) / rtk::kLeafBvh;
-    auto geo_of = [&](uint32_t k) {
-        rtk::GeoRec g;
-        if (k == rtbvh::kSentinel) {  // never-hit padding slot
-            g.cx = g.cy = g.cz = 0.0;
-            g.r2 = -std::numeric_limits<double>::infinity();
-            return g;
-        }
-        const rt_sphere& sp = ctx->spheres[k];
-        const double r = sp.radius > 0 ? sp.radius : 0.0;
-        g.cx = sp.center[0];
-        g.cy = sp.center[1];
-        g.cz = sp.center[2];
-        g.r2 = r * r;
-        return g;
-    };
-    std::vector<rtk::BvhNode> nodes(nn);
+    auto sphere = [&](uint32_t k) { return k == rtbvh::kSentinel ? nullptr : &sd.spheres[k]; };
+    sd.nodes.assign(nn, rtk::BvhNode{});
     for (size_t i = 0; i < nn; i++) {
         const rtbvh::Node& src = bvh.nodes[i];
-        rtk::BvhNode& d = nodes[i];
-        std::memset(&d, 0, sizeof d);
+        rtk::BvhNode& d = sd.nodes[i];
         for (int a = 0; a < 3; a++) {  // {lo, hi, hi, lo}: see rtk::BvhNode
             d.c0[a][0] = d.c0[a][3] = src.lo0[a];
             d.c0[a][1] = d.c0[a][2] = src.hi0[a];
@@ -183,54 +198,160 @@ int upload_bvh(rt_context* ctx, double bound) {
         d.ref0 = device_ref(src.ref0);
         d.ref1 = device_ref(src.ref1);
     }
-    std::vector<rtk::BvhLeaf> leaves(nl ? nl : 1);
+    sd.leaves.assign(nl ? nl : 1, rtk::BvhLeaf{});
     for (size_t l = 0; l < nl; l++)
         for (int u = 0; u < rtk::kLeafBvh; u++) {
             const uint32_t k = bvh.slot_to_sphere[na + l * rtk::kLeafBvh + u];
-            const rtk::GeoRec g = geo_of(k);
-            leaves[l].g[u] = rtk::LeafGeo{g.cx, g.cy, g.cz, g.r2};
-            leaves[l].sid[u] = k;
+            const rtk::GeoRec g = geo_of(sphere(k));
+            sd.leaves[l].g[u] = rtk::LeafGeo{g.cx, g.cy, g.cz, g.r2};
+            sd.leaves[l].sid[u] = k;
         }
-    std::vector<rtk::GeoRec> ageo(na ? na : 1);
-    std::vector<uint32_t> asid(na ? na : 1, 0);
+    sd.ageo.assign(na ? na : 1, geo_of(nullptr));
+    sd.asid.assign(na ? na : 1, 0);
     for (size_t q = 0; q < na; q++) {
-        ageo[q] = geo_of(bvh.slot_to_sphere[q]);
-        asid[q] = bvh.slot_to_sphere[q];
+        sd.ageo[q] = geo_of(sphere(bvh.slot_to_sphere[q]));
+        sd.asid[q] = bvh.slot_to_sphere[q];
     }
-    int rc = ensure_buffer((void**)&ctx->d_nodes, &ctx->nodes_bytes, nn * sizeof(rtk::BvhNode));
-    if (!rc) rc = ensure_buffer((void**)&ctx->d_leaves, &ctx->leaves_bytes, leaves.size() * sizeof(rtk::BvhLeaf));
-    if (!rc) rc = ensure_buffer((void**)&ctx->d_always_geo, &ctx->always_geo_bytes, ageo.size() * sizeof(rtk::GeoRec));
-    if (!rc) rc = ensure_buffer((void**)&ctx->d_always_sid, &ctx->always_sid_bytes, asid.size() * sizeof(uint32_t));
-    if (rc) return rc;
-    HIP_CHECK(hipMemcpyAsync(ctx->d_nodes, nodes.data(), nn * sizeof(rtk::BvhNode), hipMemcpyHostToDevice, ctx->stream));
-    HIP_CHECK(hipMemcpyAsync(ctx->d_leaves, leaves.data(), leaves.size() * sizeof(rtk::BvhLeaf), hipMemcpyHostToDevice,
-                             ctx->stream));
-    HIP_CHECK(hipMemcpyAsync(ctx->d_always_geo, ageo.data(), ageo.size() * sizeof(rtk::GeoRec), hipMemcpyHostToDevice,
-                             ctx->stream));
-    HIP_CHECK(hipMemcpyAsync(ctx->d_always_sid, asid.data(), asid.size() * sizeof(uint32_t), hipMemcpyHostToDevice,
-                             ctx->stream));
+    sd.n_nodes = (uint32_t)nn;
+    sd.n_leaves = (uint32_t)nl;
+    sd.n_always = (uint32_t)na;
+    sd.depth = (uint32_t)std::max(2, std::min(bvh.depth, rtk::kMaxDepthBvh));
+}
+
+// Device records + BVH of a sphere list (validated by the caller).
+void build_scene(const rt_sphere* spheres, size_t n, SceneData& sd) {
+    sd = SceneData{};
+    sd.spheres.assign(spheres, spheres + n);
+    const size_t n_pad = (n + rtk::kPad - 1) / rtk::kPad * rtk::kPad;
+    sd.geo.assign(n_pad, geo_of(nullptr));
+    sd.mat.assign(n, rtk::MatRec{});
+    for (size_t k = 0; k < n; k++) {
+        sd.geo[k] = geo_of(&spheres[k]);
+        rtk::MatRec& m = sd.mat[k];
+        const double r = spheres[k].radius > 0 ? spheres[k].radius : 0.0;
+        for (int c = 0; c < 3; c++) m.albedo[c] = spheres[k].albedo[c];
+        m.fuzz = spheres[k].fuzz;
+        m.ior = spheres[k].refraction_index;
+        m.inv_r = 1.0 / r;
+        const double ior = spheres[k].refraction_index;
+        m.inv_ior = 1.0 / ior;
+        for (int face = 0; face < 2; face++) {  // reflectance()'s r0 (material.zig:106-108) per face
+            const double ri = face == 0 ? m.inv_ior : ior;
+            double r0 = (1 - ri) / (1 + ri);
+            r0 = r0 * r0;
+            (face == 0 ? m.r0_front : m.r0_back) = r0;
+        }
+        m.kind = spheres[k].material;
+    }
+    const double extent = rtbvh::scene_extent(spheres, n);
+    build_bvh(sd, extent * (1.0 + 0x1p-20) + 1e-300);
+}
+
+bool same_spheres(const SceneData& sd, const rt_sphere* s, size_t n) {
+    return sd.spheres.size() == n && n && std::memcmp(sd.spheres.data(), s, n * sizeof(rt_sphere)) == 0;
+}
+
+// Waits until the device has finished the context's last render (before rewriting its buffers).
+int quiesce(rt_context* ctx) {
+    if (ctx->done_valid) HIP_CHECK(hipEventSynchronize(ctx->done));
     HIP_CHECK(hipStreamSynchronize(ctx->stream));
-    ctx->bvh.nodes = ctx->d_nodes;
-    ctx->bvh.leaves = ctx->d_leaves;
-    ctx->bvh.always_geo = ctx->d_always_geo;
-    ctx->bvh.always_sid = ctx->d_always_sid;
-    ctx->bvh.n_nodes = (uint32_t)nn;
-    ctx->bvh.n_leaves = (uint32_t)nl;
-    ctx->bvh.n_always = (uint32_t)na;
-    ctx->bvh.stack_depth = (uint32_t)std::max(2, std::min(bvh.depth, rtk::kMaxDepthBvh));
     return RT_OK;
 }
 
-// Walk selection: RTZIG_KERNEL names a linear variant (lds_u*, smem_u*) or "bvh"; default: the
+int ensure_buffer(rt_context* ctx, void** ptr, size_t* bytes, size_t need) {
+    if (*ptr && *bytes >= need) return RT_OK;
+    int rc = quiesce(ctx);
+    if (rc) return rc;
+    (void)hipFree(*ptr);
+    *ptr = nullptr;
+    *bytes = 0;
+    hipError_t e = hipMalloc(ptr, need ? need : 1);
+    if (e != hipSuccess) return hip_fail(e, "hipMalloc(workspace)");
+    *bytes = need;
+    return RT_OK;
+}
+
+template <class T>
+int upload(rt_context* ctx, T** dptr, size_t* bytes, const std::vector<T>& v) {
+    int rc = ensure_buffer(ctx, (void**)dptr, bytes, v.size() * sizeof(T));
+    if (rc) return rc;
+    HIP_CHECK(hipMemcpyAsync(*dptr, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, ctx->stream));
+    return RT_OK;
+}
+
+int upload_bvh(rt_context* ctx) {
+    const SceneData& sd = ctx->scene;
+    if (!sd.bvh_ok) return RT_OK;
+    int rc = quiesce(ctx);
+    if (!rc) rc = upload(ctx, &ctx->d_nodes, &ctx->nodes_bytes, sd.nodes);
+    if (!rc) rc = upload(ctx, &ctx->d_leaves, &ctx->leaves_bytes, sd.leaves);
+    if (!rc) rc = upload(ctx, &ctx->d_always_geo, &ctx->always_geo_bytes, sd.ageo);
+    if (!rc) rc = upload(ctx, &ctx->d_always_sid, &ctx->always_sid_bytes, sd.asid);
+    if (rc) return rc;
+    HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    rtk::BvhArgs& b = ctx->bvh;
+    b = rtk::BvhArgs{};
+    b.nodes = ctx->d_nodes;
+    b.leaves = ctx->d_leaves;
+    b.always_geo = ctx->d_always_geo;
+    b.always_sid = ctx->d_always_sid;
+    b.n_nodes = sd.n_nodes;
+    b.n_leaves = sd.n_leaves;
+    b.n_always = sd.n_always;
+    b.stack_depth = sd.depth;
+    float ob = (float)sd.origin_bound;  // rounded down: a lane counts as "far" no later than the padding allows
+    if ((double)ob > sd.origin_bound) ob = std::nextafterf(ob, 0.0f);
+    // test hook: RTZIG_BVH_ORIGIN_SCALE=<s> < 1 marks lanes "far" early, so the tests can check the
+    // no-culling walk of far-origin lanes against the oracle on rays that do hit spheres
+    if (const char* e = std::getenv("RTZIG_BVH_ORIGIN_SCALE")) ob = (float)(ob * std::min(1.0, std::atof(e)));
+    b.origin_bound = ob;
+    return RT_OK;
+}
+
+// Uploads a host scene to the context's device (a copy stays on the host side of the context).
+int upload_scene(rt_context* ctx, const SceneData& sd) {
+    HIP_CHECK(hipSetDevice(ctx->device));
+    int rc = quiesce(ctx);
+    if (rc) return rc;
+    const size_t n_pad = sd.geo.size(), n = sd.mat.size();
+    if (n_pad > ctx->capacity) {
+        (void)hipFree(ctx->d_geo);
+        (void)hipFree(ctx->d_mat);
+        ctx->d_geo = nullptr;
+        ctx->d_mat = nullptr;
+        ctx->capacity = 0;
+        HIP_CHECK(hipMalloc(&ctx->d_geo, n_pad * sizeof(rtk::GeoRec)));
+        HIP_CHECK(hipMalloc(&ctx->d_mat, n_pad * sizeof(rtk::MatRec)));
+        ctx->capacity = (uint32_t)n_pad;
+    }
+    HIP_CHECK(hipMemcpyAsync(ctx->d_geo, sd.geo.data(), n_pad * sizeof(rtk::GeoRec), hipMemcpyHostToDevice, ctx->stream));
+    HIP_CHECK(hipMemcpyAsync(ctx->d_mat, sd.mat.data(), n * sizeof(rtk::MatRec), hipMemcpyHostToDevice, ctx->stream));
+    HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    ctx->n_spheres = (uint32_t)n;
+    ctx->scene = sd;
+    return upload_bvh(ctx);
+}
+
+// Walk selection: RTZIG_KERNEL names a linear variant (lds_u4, smem_u4) or "bvh"; default: the
 // BVH walk when it built, else the linear default variant.
 bool use_bvh(const rt_context* ctx) {
     const char* e = std::getenv("RTZIG_KERNEL");
     if (e && std::strncmp(e, "bvh", 3) != 0) return false;
-    return ctx->bvh_ok;
+    return ctx->scene.bvh_ok;
 }
 
-rtk::KernelParams make_params(const rt_camera* c, uint32_t fmt, uint32_t row0, uint32_t row_step,
-                              uint32_t n_rows, uint32_t n_spheres) {
+// The chunk schedule of rt_kernel.h "Work units" for `spp` samples.
+void unit_schedule(uint32_t spp, rtk::UnitArgs& ua) {
+    ua.n_main = spp > rtk::kUnitS ? (spp - rtk::kUnitS) / rtk::kUnitS : 0;
+    ua.tail_r = spp - ua.n_main * rtk::kUnitS;
+    uint32_t t = 0;
+    while ((1u << t) < ua.tail_r) ++t;
+    ua.tail_t = t;
+    ua.n_chunks = ua.n_main + t + 1;
+}
+
+rtk::KernelParams make_params(const rt_camera* c, uint32_t row0, uint32_t row_step, uint32_t n_rows,
+                              uint32_t n_spheres) {
     rtk::KernelParams p;
     std::memset(&p, 0, sizeof p);
     p.width = c->image_width;
@@ -266,8 +387,11 @@ rtk::KernelParams make_params(const rt_camera* c, uint32_t fmt, uint32_t row0, u
     p.n_pad = (n_spheres + rtk::kPad - 1) / rtk::kPad * rtk::kPad;
     p.div_layer = rtk::fastdiv_make(n_rows * c->image_width);  // < 2^32 pixels (checked by callers)
     p.div_width = rtk::fastdiv_make(c->image_width);
-    (void)fmt;
     return p;
+}
+
+hipError_t make_event(hipEvent_t* e, bool timed) {
+    return timed ? hipEventCreate(e) : hipEventCreateWithFlags(e, hipEventDisableTiming);
 }
 
 }  // namespace
@@ -293,9 +417,14 @@ int rt_context_create(int device, rt_context** out_ctx) {
     auto* ctx = new rt_context;
     ctx->device = device;
     hipError_t e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = make_event(&ctx->done, false);
+    int cus = 0;
+    if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
+    ctx->ring_waves = (uint32_t)std::max(cus, 1) * kMaxWavesPerCU;
     if (e != hipSuccess) {
-        delete ctx;
-        return hip_fail(e, "hipStreamCreate");
+        const int rc = hip_fail(e, "rt_context_create: stream / event");
+        rt_context_destroy(ctx);
+        return rc;
     }
     *out_ctx = ctx;
     return RT_OK;
@@ -304,17 +433,16 @@ int rt_context_create(int device, rt_context** out_ctx) {
 int rt_context_destroy(rt_context* ctx) {
     if (!ctx) return RT_OK;
     (void)hipSetDevice(ctx->device);
+    if (ctx->done_valid) (void)hipEventSynchronize(ctx->done);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
-    (void)hipFree(ctx->d_geo);
-    (void)hipFree(ctx->d_mat);
-    (void)hipFree(ctx->d_samples);
-    (void)hipFree(ctx->d_sums);
-    (void)hipFree(ctx->d_queue);
-    (void)hipFree(ctx->d_nodes);
-    (void)hipFree(ctx->d_leaves);
-    (void)hipFree(ctx->d_always_geo);
-    (void)hipFree(ctx->d_always_sid);
+    for (void* p : {(void*)ctx->d_geo, (void*)ctx->d_mat, (void*)ctx->d_ring, (void*)ctx->d_sums, (void*)ctx->d_flags,
+                    (void*)ctx->d_ctr, (void*)ctx->d_nodes, (void*)ctx->d_leaves, (void*)ctx->d_always_geo,
+                    (void*)ctx->d_always_sid, ctx->d_out, (void*)ctx->d_stats})
+        (void)hipFree(p);
+    if (ctx->h_out) (void)hipHostFree(ctx->h_out);
+    if (ctx->h_stats) (void)hipHostFree(ctx->h_stats);
     for (hipEvent_t e : ctx->events) (void)hipEventDestroy(e);
+    if (ctx->done) (void)hipEventDestroy(ctx->done);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
     return RT_OK;
@@ -324,52 +452,23 @@ int rt_context_set_scene(rt_context* ctx, const rt_sphere* spheres, size_t n) {
     if (!ctx) { rt_set_last_error("null context"); return RT_ERR_INVALID; }
     int rc = validate_spheres(spheres, n);
     if (rc) return rc;
+    SceneData sd;
+    build_scene(spheres, n, sd);
+    return upload_scene(ctx, sd);
+}
+
+int rt_context_sync(rt_context* ctx) {
+    if (!ctx) { rt_set_last_error("null context"); return RT_ERR_INVALID; }
     HIP_CHECK(hipSetDevice(ctx->device));
-    const size_t n_pad = (n + rtk::kPad - 1) / rtk::kPad * rtk::kPad;
-    std::vector<rtk::GeoRec> geo(n_pad);
-    std::vector<rtk::MatRec> mat(n);
-    for (size_t k = n; k < n_pad; k++) {  // never-hit sentinels (rt_kernel.h)
-        geo[k].cx = geo[k].cy = geo[k].cz = 0.0;
-        geo[k].r2 = -std::numeric_limits<double>::infinity();
+    int rc = quiesce(ctx);
+    if (rc || !ctx->d_ctr) return rc;
+    unsigned long long err = 0;
+    HIP_CHECK(hipMemcpy(&err, ctx->d_ctr + 8, sizeof err, hipMemcpyDeviceToHost));
+    if (err) {
+        rt_set_last_error("render kernel: a wave timed out waiting for a running-sum hand-off");
+        return RT_ERR_HIP;
     }
-    for (size_t k = 0; k < n; k++) {
-        const double r = spheres[k].radius > 0 ? spheres[k].radius : 0.0;  // sphere.zig:21
-        geo[k].cx = spheres[k].center[0];
-        geo[k].cy = spheres[k].center[1];
-        geo[k].cz = spheres[k].center[2];
-        geo[k].r2 = r * r;
-        std::memset(&mat[k], 0, sizeof mat[k]);
-        for (int c = 0; c < 3; c++) mat[k].albedo[c] = spheres[k].albedo[c];
-        mat[k].fuzz = spheres[k].fuzz;
-        mat[k].ior = spheres[k].refraction_index;
-        mat[k].inv_r = 1.0 / r;
-        const double ior = spheres[k].refraction_index;
-        mat[k].inv_ior = 1.0 / ior;
-        for (int face = 0; face < 2; face++) {  // reflectance()'s r0 (material.zig:106-108) per face
-            const double ri = face == 0 ? mat[k].inv_ior : ior;
-            double r0 = (1 - ri) / (1 + ri);
-            r0 = r0 * r0;
-            (face == 0 ? mat[k].r0_front : mat[k].r0_back) = r0;
-        }
-        mat[k].kind = spheres[k].material;
-    }
-    if (n_pad > ctx->capacity) {
-        (void)hipFree(ctx->d_geo);
-        (void)hipFree(ctx->d_mat);
-        ctx->d_geo = nullptr;
-        ctx->d_mat = nullptr;
-        ctx->capacity = 0;
-        HIP_CHECK(hipMalloc(&ctx->d_geo, n_pad * sizeof(rtk::GeoRec)));
-        HIP_CHECK(hipMalloc(&ctx->d_mat, n_pad * sizeof(rtk::MatRec)));
-        ctx->capacity = (uint32_t)n_pad;
-    }
-    HIP_CHECK(hipMemcpyAsync(ctx->d_geo, geo.data(), n_pad * sizeof(rtk::GeoRec), hipMemcpyHostToDevice, ctx->stream));
-    HIP_CHECK(hipMemcpyAsync(ctx->d_mat, mat.data(), n * sizeof(rtk::MatRec), hipMemcpyHostToDevice, ctx->stream));
-    HIP_CHECK(hipStreamSynchronize(ctx->stream));
-    ctx->n_spheres = (uint32_t)n;
-    ctx->spheres.assign(spheres, spheres + n);
-    const double extent = rtbvh::scene_extent(spheres, n);
-    return upload_bvh(ctx, extent * (1.0 + 0x1p-20) + 1e-300);
+    return RT_OK;
 }
 
 int rt_render_rows_async(rt_context* ctx, const rt_camera* cam, uint32_t output_format, uint32_t row0,
@@ -390,82 +489,91 @@ int rt_render_rows_async(rt_context* ctx, const rt_camera* cam, uint32_t output_
     HIP_CHECK(hipSetDevice(ctx->device));
     hipStream_t s = (hipStream_t)stream;  // NULL = the HIP null stream, like torch's default stream
 
-    // Chunk the samples so that [s_count][P][3] doubles fit the workspace budget.
-    const uint64_t P = (uint64_t)n_rows * cam->image_width;
-    const uint64_t layer = P * 3 * sizeof(double);
-    // (the free-memory query is skipped when the whole frame fits the workspace already allocated)
-    const bool fits = ctx->d_samples && ctx->samples_bytes / layer >= cam->samples_per_pixel;
-    uint64_t s_chunk = fits ? cam->samples_per_pixel : workspace_budget() / layer;
-    if (s_chunk < 1) s_chunk = 1;
-    if (s_chunk > cam->samples_per_pixel) s_chunk = cam->samples_per_pixel;
-    if (s_chunk * P > 0xffffffffULL) s_chunk = 0xffffffffULL / P;  // kernel item index is 32-bit
-    const uint32_t n_chunks = (uint32_t)((cam->samples_per_pixel + s_chunk - 1) / s_chunk);
-    rc = ensure_buffer((void**)&ctx->d_samples, &ctx->samples_bytes, s_chunk * layer);
-    if (!rc && n_chunks > 1) rc = ensure_buffer((void**)&ctx->d_sums, &ctx->sums_bytes, layer);
-    if (!rc && !ctx->d_queue) {
-        size_t qb = 0;
-        rc = ensure_buffer((void**)&ctx->d_queue, &qb, rtk::kQueueBufferBytes);
-    }
-    if (rc) return rc;
-
-    if (ctx->timing) {
-        if (ctx->log_used + n_chunks > kMaxTimedChunks) ctx->log_used = 0;  // wrap: totals restart
-        ctx->call_first = ctx->log_used;
-        ctx->log_used += n_chunks;
-        while (ctx->events.size() < 4 * (size_t)ctx->log_used) {
-            hipEvent_t e;
-            HIP_CHECK(hipEventCreate(&e));
-            ctx->events.push_back(e);
-        }
-        ctx->timed_chunks = n_chunks;
-    }
     // camera-ray origins (center + defocus disk) must lie inside the BVH padding's origin bound
+    // (lanes outside it would walk without culling: correct, but every camera ray would pay)
     double cam_bound = 0;
     for (int a = 0; a < 3; a++)
         cam_bound = std::max(cam_bound, std::fabs(cam->center[a]) + std::fabs(cam->defocus_disk_u[a]) +
                                             std::fabs(cam->defocus_disk_v[a]));
-    if (ctx->bvh_ok && !(cam_bound <= ctx->bvh_origin_bound)) {
-        rc = upload_bvh(ctx, std::max(cam_bound, ctx->bvh_origin_bound) * 1.01);
+    if (ctx->scene.bvh_ok && !(cam_bound <= ctx->scene.origin_bound)) {
+        rc = quiesce(ctx);  // the previous render may still walk the old tree
+        if (rc) return rc;
+        build_bvh(ctx->scene, std::max(cam_bound, ctx->scene.origin_bound) * 1.01);
+        rc = upload_bvh(ctx);
         if (rc) return rc;
     }
-    const bool bvh = use_bvh(ctx);
-    rtk::KernelParams p = make_params(cam, output_format, row0, row_step, n_rows, ctx->n_spheres);
-    p.prof = ctx->profile && d_stats ? 1u : 0u;
-    if (const char* e = std::getenv("RTZIG_ORDER"))
-        p.order = std::strcmp(e, "pixel") == 0 ? 1u : (std::strcmp(e, "tile") == 0 ? 2u : 0u);
-    for (uint32_t c = 0; c < n_chunks; c++) {
-        p.s_begin = (uint32_t)(c * s_chunk);
-        p.s_count = (uint32_t)std::min<uint64_t>(s_chunk, cam->samples_per_pixel - p.s_begin);
-        if (ctx->timing) HIP_CHECK(hipEventRecord(ctx->events[4 * (ctx->call_first + c) + 0], s));
-        if (bvh && ctx->precision == RT_PRECISION_F32)
-            HIP_CHECK(rtk_launch_samples_fast(&p, &ctx->bvh, ctx->d_geo, ctx->d_mat, ctx->d_samples, ctx->d_queue,
-                                              d_stats, s, &ctx->last_kernel));
-        else if (bvh)
-            HIP_CHECK(rtk_launch_samples_bvh(&p, &ctx->bvh, ctx->d_geo, ctx->d_mat, ctx->d_samples, ctx->d_queue,
-                                             d_stats, s, &ctx->last_kernel));
-        else
-            HIP_CHECK(rtk_launch_samples(&p, ctx->d_geo, ctx->d_mat, ctx->d_samples, ctx->d_queue, d_stats, s,
-                                         &ctx->last_kernel));
-        if (ctx->timing) HIP_CHECK(hipEventRecord(ctx->events[4 * (ctx->call_first + c) + 1], s));
-        rtk::ReduceParams rp;
-        std::memset(&rp, 0, sizeof rp);
-        rp.n_pixels = (uint32_t)P;
-        rp.s_count = p.s_count;
-        rp.first = c == 0;
-        rp.last = c + 1 == n_chunks;
-        rp.out_format = output_format;
-        rp.scale = cam->pixel_samples_scale;
-        if (ctx->timing) HIP_CHECK(hipEventRecord(ctx->events[4 * (ctx->call_first + c) + 2], s));
-        HIP_CHECK(rtk_launch_reduce(&rp, ctx->d_samples, ctx->d_sums, d_out, s));
-        if (ctx->timing) HIP_CHECK(hipEventRecord(ctx->events[4 * (ctx->call_first + c) + 3], s));
+
+    const uint64_t P = (uint64_t)n_rows * cam->image_width;
+    rtk::UnitArgs ua;
+    std::memset(&ua, 0, sizeof ua);
+    unit_schedule(cam->samples_per_pixel, ua);
+    const uint64_t n_tiles = (P + 63) / 64;
+    if (n_tiles * ua.n_chunks >= (1ull << 32)) {
+        rt_set_last_error("too many work units (rows x samples): render fewer rows per call");
+        return RT_ERR_CAPACITY;
     }
+    rc = ensure_buffer(ctx, (void**)&ctx->d_ring, &ctx->ring_bytes,
+                       (size_t)ctx->ring_waves * rtk::kRingWaveDoubles * sizeof(double));
+    if (!rc && ua.n_chunks > 1) rc = ensure_buffer(ctx, (void**)&ctx->d_sums, &ctx->sums_bytes, P * 3 * sizeof(double));
+    const size_t flag_bytes = (n_tiles * sizeof(uint32_t) + 15) & ~(size_t)15;  // memset in 16-B multiples
+    if (!rc) rc = ensure_buffer(ctx, (void**)&ctx->d_flags, &ctx->flags_bytes, flag_bytes);
+    if (!rc && !ctx->d_ctr) {
+        size_t cb = 0;
+        rc = ensure_buffer(ctx, (void**)&ctx->d_ctr, &cb, rtk::kCtrBytes);
+    }
+    if (rc) return rc;
+    ua.ring = ctx->d_ring;
+    ua.sums = ctx->d_sums;
+    ua.flags = ctx->d_flags;
+    ua.out = d_out;
+    ua.ctr = ctx->d_ctr;
+    ua.n_tiles = (uint32_t)n_tiles;
+    ua.n_units = (uint32_t)(n_tiles * ua.n_chunks);
+    ua.div_tiles = rtk::fastdiv_make((uint32_t)n_tiles);
+    ua.P = (uint32_t)P;
+    ua.out_format = output_format;
+    ua.ring_waves = ctx->ring_waves;
+    ua.scale = cam->pixel_samples_scale;
+
+    if (ctx->timing) {
+        if (ctx->log_used + 1 > kMaxTimed) ctx->log_used = 0;  // wrap: totals restart
+        ctx->call_first = ctx->log_used;
+        ctx->log_used += 1;
+        while (ctx->events.size() < 2 * (size_t)ctx->log_used) {
+            hipEvent_t e;
+            HIP_CHECK(make_event(&e, true));
+            ctx->events.push_back(e);
+        }
+        ctx->timed_calls = 1;
+    }
+    // a previous render of this context on another stream may still use the buffers
+    if (ctx->done_valid && ctx->done_stream != s) HIP_CHECK(hipStreamWaitEvent(s, ctx->done, 0));
+    HIP_CHECK(hipMemsetAsync(ctx->d_ctr, 0, rtk::kCtrBytes, s));
+    HIP_CHECK(hipMemsetAsync(ctx->d_flags, 0, flag_bytes, s));
+    const bool bvh = use_bvh(ctx);
+    rtk::KernelParams p = make_params(cam, row0, row_step, n_rows, ctx->n_spheres);
+    p.prof = ctx->profile && d_stats ? 1u : 0u;
+    p.s_begin = 0;
+    p.s_count = cam->samples_per_pixel;
+    hipEvent_t* ev = ctx->timing ? &ctx->events[2 * ctx->call_first] : nullptr;
+    if (ev) HIP_CHECK(hipEventRecord(ev[0], s));
+    if (bvh && ctx->precision == RT_PRECISION_F32)
+        HIP_CHECK(rtk_launch_samples_fast(&p, &ctx->bvh, ctx->d_geo, ctx->d_mat, &ua, d_stats, s, &ctx->last_kernel));
+    else if (bvh)
+        HIP_CHECK(rtk_launch_samples_bvh(&p, &ctx->bvh, ctx->d_geo, ctx->d_mat, &ua, d_stats, s, &ctx->last_kernel));
+    else
+        HIP_CHECK(rtk_launch_samples(&p, ctx->d_geo, ctx->d_mat, &ua, d_stats, s, &ctx->last_kernel));
+    if (ev) HIP_CHECK(hipEventRecord(ev[1], s));
+    HIP_CHECK(hipEventRecord(ctx->done, s));
+    ctx->done_valid = true;
+    ctx->done_stream = s;
     return RT_OK;
 }
 
 int rt_context_enable_timing(rt_context* ctx, int enable) {
     if (!ctx) { rt_set_last_error("null context"); return RT_ERR_INVALID; }
     ctx->timing = enable != 0;
-    ctx->timed_chunks = 0;
+    ctx->timed_calls = 0;
     ctx->call_first = 0;
     ctx->log_used = 0;
     return RT_OK;
@@ -487,44 +595,88 @@ int rt_context_enable_profile(rt_context* ctx, int enable) {
     return RT_OK;
 }
 
-int rt_context_kernel_times(rt_context* ctx, double* sample_ms, double* reduce_ms) {
-    if (!ctx) { rt_set_last_error("null context"); return RT_ERR_INVALID; }
-    if (!ctx->timing || ctx->timed_chunks == 0) { rt_set_last_error("timing not enabled or nothing rendered"); return RT_ERR_INVALID; }
+static int sum_times(rt_context* ctx, uint32_t first, uint32_t count, double* sample_ms, double* reduce_ms) {
     HIP_CHECK(hipSetDevice(ctx->device));
-    double sm = 0, rm = 0;
-    for (uint32_t c = ctx->call_first; c < ctx->call_first + ctx->timed_chunks; c++) {
-        float a = 0, b = 0;
-        HIP_CHECK(hipEventSynchronize(ctx->events[4 * c + 3]));
-        HIP_CHECK(hipEventElapsedTime(&a, ctx->events[4 * c + 0], ctx->events[4 * c + 1]));
-        HIP_CHECK(hipEventElapsedTime(&b, ctx->events[4 * c + 2], ctx->events[4 * c + 3]));
+    double sm = 0;
+    for (uint32_t c = first; c < first + count; c++) {
+        float a = 0;
+        HIP_CHECK(hipEventSynchronize(ctx->events[2 * c + 1]));
+        HIP_CHECK(hipEventElapsedTime(&a, ctx->events[2 * c + 0], ctx->events[2 * c + 1]));
         sm += a;
-        rm += b;
     }
     if (sample_ms) *sample_ms = sm;
-    if (reduce_ms) *reduce_ms = rm;
+    if (reduce_ms) *reduce_ms = 0.0;  // no reduce pass: the sample kernel accumulates in order itself
     return RT_OK;
 }
 
-int rt_context_kernel_times_total(rt_context* ctx, double* sample_ms, double* reduce_ms, uint32_t* n_chunks) {
+int rt_context_kernel_times(rt_context* ctx, double* sample_ms, double* reduce_ms) {
+    if (!ctx) { rt_set_last_error("null context"); return RT_ERR_INVALID; }
+    if (!ctx->timing || ctx->timed_calls == 0) { rt_set_last_error("timing not enabled or nothing rendered"); return RT_ERR_INVALID; }
+    return sum_times(ctx, ctx->call_first, ctx->timed_calls, sample_ms, reduce_ms);
+}
+
+int rt_context_kernel_times_total(rt_context* ctx, double* sample_ms, double* reduce_ms, uint32_t* n_launches) {
     if (!ctx) { rt_set_last_error("null context"); return RT_ERR_INVALID; }
     if (!ctx->timing) { rt_set_last_error("timing not enabled"); return RT_ERR_INVALID; }
-    HIP_CHECK(hipSetDevice(ctx->device));
-    double sm = 0, rm = 0;
-    for (uint32_t c = 0; c < ctx->log_used; c++) {
-        float a = 0, b = 0;
-        HIP_CHECK(hipEventSynchronize(ctx->events[4 * c + 3]));
-        HIP_CHECK(hipEventElapsedTime(&a, ctx->events[4 * c + 0], ctx->events[4 * c + 1]));
-        HIP_CHECK(hipEventElapsedTime(&b, ctx->events[4 * c + 2], ctx->events[4 * c + 3]));
-        sm += a;
-        rm += b;
-    }
-    if (sample_ms) *sample_ms = sm;
-    if (reduce_ms) *reduce_ms = rm;
-    if (n_chunks) *n_chunks = ctx->log_used;
+    const int rc = sum_times(ctx, 0, ctx->log_used, sample_ms, reduce_ms);
+    if (rc) return rc;
+    if (n_launches) *n_launches = ctx->log_used;
     return RT_OK;
 }
 
 const char* rt_kernel_name(rt_context* ctx) { return ctx ? ctx->last_kernel : "render_kernel"; }
+
+}  // extern "C"
+
+// ------------------------------------------------------------------------------------------------
+// rt_render: the blocking drop-in for Camera.render, over process-wide cached contexts
+// ------------------------------------------------------------------------------------------------
+namespace {
+
+std::mutex g_cache_mu;             // guards g_cache and serialises rt_render calls
+std::vector<rt_context*> g_cache;  // one context per device ordinal (created on first use)
+
+// Gets (creating if needed) the cached contexts of devices [first, first + G) and makes each hold
+// `spheres`: contexts are created on parallel host threads; the scene is built on the host once
+// per call at most and uploaded only where it differs.
+int cached_contexts(int first, int G, const rt_sphere* spheres, size_t n, std::vector<rt_context*>& out) {
+    if ((int)g_cache.size() < first + G) g_cache.resize(first + G, nullptr);
+    bool need_scene = false;
+    for (int g = 0; g < G; g++) {
+        const rt_context* c = g_cache[first + g];
+        need_scene = need_scene || !c || !same_spheres(c->scene, spheres, n);
+    }
+    SceneData sd;
+    if (need_scene) build_scene(spheres, n, sd);
+    std::vector<int> rcs(G, RT_OK);
+    std::vector<std::string> msgs(G);
+    auto work = [&](int g) {
+        rt_context*& c = g_cache[first + g];
+        int rc = RT_OK;
+        if (!c) rc = rt_context_create(first + g, &c);
+        if (!rc && !same_spheres(c->scene, spheres, n)) rc = upload_scene(c, sd);
+        rcs[g] = rc;
+        if (rc) msgs[g] = rt_last_error();  // thread-local: carried back to the caller's thread
+    };
+    if (G == 1) {
+        work(0);
+    } else {
+        std::vector<std::thread> th;
+        for (int g = 0; g < G; g++) th.emplace_back(work, g);
+        for (auto& t : th) t.join();
+    }
+    for (int g = 0; g < G; g++)
+        if (rcs[g]) {
+            rt_set_last_error(msgs[g]);
+            return rcs[g];
+        }
+    out.assign(g_cache.begin() + first, g_cache.begin() + first + G);
+    return RT_OK;
+}
+
+}  // namespace
+
+extern "C" {
 
 int rt_render(const rt_camera* cam, const rt_sphere* spheres, size_t n, const rt_options* opts, void* out) {
     int rc = validate_camera(cam);
@@ -557,73 +709,82 @@ int rt_render(const rt_camera* cam, const rt_sphere* spheres, size_t n, const rt
     G = std::min<int>(G, (int)H);
     const size_t px_bytes = o.output_format == RT_OUT_LINEAR_F64 ? 3 * sizeof(double) : 3;
 
-    struct Dev {
-        rt_context* ctx = nullptr;
-        void* d_out = nullptr;
-        uint64_t* d_stats = nullptr;
-        std::vector<uint8_t> host;
-        uint32_t n_rows = 0;
-    };
-    std::vector<Dev> devs(G);
-    auto cleanup = [&]() {
-        for (auto& d : devs) {
-            if (!d.ctx) continue;
-            (void)hipSetDevice(d.ctx->device);
-            (void)hipFree(d.d_out);
-            (void)hipFree(d.d_stats);
-            rt_context_destroy(d.ctx);
-        }
-    };
+    std::lock_guard<std::mutex> lock(g_cache_mu);
+    std::vector<rt_context*> ctxs;
+    rc = cached_contexts(first, G, spheres, n, ctxs);
+    if (rc) return rc;
+    std::vector<uint32_t> rows(G);
     for (int g = 0; g < G; g++) {
-        Dev& d = devs[g];
-        rc = rt_context_create(first + g, &d.ctx);
-        if (!rc) rc = rt_context_set_scene(d.ctx, spheres, n);
-        if (!rc) rc = rt_context_set_precision(d.ctx, (int)o.precision);
-        if (rc) { cleanup(); return rc; }
-        d.n_rows = (H - (uint32_t)g + (uint32_t)G - 1) / (uint32_t)G;
-        const size_t bytes = (size_t)d.n_rows * W * px_bytes;
-        hipError_t e = hipMalloc(&d.d_out, bytes ? bytes : 1);
-        if (e == hipSuccess) e = hipMalloc((void**)&d.d_stats, 2 * sizeof(uint64_t));
-        if (e == hipSuccess) e = hipMemsetAsync(d.d_stats, 0, 2 * sizeof(uint64_t), d.ctx->stream);
-        if (e != hipSuccess) { cleanup(); return hip_fail(e, "hipMalloc"); }
-        rc = rt_render_rows_async(d.ctx, cam, o.output_format, (uint32_t)g, (uint32_t)G, d.n_rows,
-                                  d.d_out, d.d_stats, d.ctx->stream);
-        if (rc) { cleanup(); return rc; }
+        rt_context* c = ctxs[g];
+        HIP_CHECK(hipSetDevice(c->device));
+        rc = rt_context_set_precision(c, (int)o.precision);
+        rows[g] = (H - (uint32_t)g + (uint32_t)G - 1) / (uint32_t)G;
+        const size_t bytes = (size_t)rows[g] * W * px_bytes;
+        if (!rc) rc = ensure_buffer(c, &c->d_out, &c->d_out_bytes, bytes);
+        if (!rc && !c->d_stats) {
+            size_t sb = 0;
+            rc = ensure_buffer(c, (void**)&c->d_stats, &sb, 2 * sizeof(uint64_t));
+        }
+        if (rc) return rc;
+        if (c->h_out_bytes < bytes) {
+            if (c->h_out) (void)hipHostFree(c->h_out);
+            c->h_out = nullptr;
+            c->h_out_bytes = 0;
+            HIP_CHECK(hipHostMalloc(&c->h_out, bytes, hipHostMallocDefault));
+            c->h_out_bytes = bytes;
+        }
+        if (!c->h_stats) HIP_CHECK(hipHostMalloc((void**)&c->h_stats, 3 * sizeof(uint64_t), hipHostMallocDefault));
+        HIP_CHECK(hipMemsetAsync(c->d_stats, 0, 2 * sizeof(uint64_t), c->stream));
+        rc = rt_render_rows_async(c, cam, o.output_format, (uint32_t)g, (uint32_t)G, rows[g], c->d_out, c->d_stats,
+                                  c->stream);
+        if (rc) return rc;
+        HIP_CHECK(hipMemcpyAsync(c->h_out, c->d_out, bytes, hipMemcpyDeviceToHost, c->stream));
+        HIP_CHECK(hipMemcpyAsync(c->h_stats, c->d_stats, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
+        HIP_CHECK(hipMemcpyAsync(c->h_stats + 2, c->d_ctr + 8, sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
     }
     uint64_t stats[2] = {0, 0};
     for (int g = 0; g < G; g++) {
-        Dev& d = devs[g];
-        (void)hipSetDevice(d.ctx->device);
-        d.host.resize((size_t)d.n_rows * W * px_bytes);
-        uint64_t st[2] = {0, 0};
-        hipError_t e = hipMemcpyAsync(d.host.data(), d.d_out, d.host.size(), hipMemcpyDeviceToHost, d.ctx->stream);
-        if (e == hipSuccess) e = hipMemcpyAsync(st, d.d_stats, sizeof st, hipMemcpyDeviceToHost, d.ctx->stream);
-        if (e == hipSuccess) e = hipStreamSynchronize(d.ctx->stream);
-        if (e != hipSuccess) { cleanup(); return hip_fail(e, "render/copy-back"); }
-        stats[0] += st[0];
-        stats[1] += st[1];
+        rt_context* c = ctxs[g];
+        HIP_CHECK(hipSetDevice(c->device));
+        HIP_CHECK(hipStreamSynchronize(c->stream));
+        if (c->h_stats[2]) {
+            rt_set_last_error("render kernel: a wave timed out waiting for a running-sum hand-off");
+            return RT_ERR_HIP;
+        }
+        stats[0] += c->h_stats[0];
+        stats[1] += c->h_stats[1];
         // un-interleave rows j = g + k*G into the caller's framebuffer
-        for (uint32_t k = 0; k < d.n_rows; k++) {
+        const uint8_t* src8 = (const uint8_t*)c->h_out;
+        for (uint32_t k = 0; k < rows[g]; k++) {
             const uint32_t j = (uint32_t)g + k * (uint32_t)G;
             if (o.output_format == RT_OUT_RGB8) {
-                std::memcpy((uint8_t*)out + (size_t)j * W * 3, d.host.data() + (size_t)k * W * 3, (size_t)W * 3);
+                std::memcpy((uint8_t*)out + (size_t)j * W * 3, src8 + (size_t)k * W * 3, (size_t)W * 3);
             } else {
-                const double* src = (const double*)d.host.data() + (size_t)k * W * 3;
+                const double* src = (const double*)c->h_out + (size_t)k * W * 3;
                 double* dst = (double*)out + (size_t)j * W * stride;
                 if (stride == 3) {
                     std::memcpy(dst, src, (size_t)W * 3 * sizeof(double));
                 } else {
                     for (uint32_t i = 0; i < W; i++)
-                        for (int c = 0; c < 3; c++) dst[(size_t)i * stride + c] = src[3 * (size_t)i + c];
+                        for (int ch = 0; ch < 3; ch++) dst[(size_t)i * stride + ch] = src[3 * (size_t)i + ch];
                 }
             }
         }
     }
-    cleanup();
     if (o.stats_out) {
         o.stats_out[0] = stats[0];
         o.stats_out[1] = stats[1];
     }
+    return RT_OK;
+}
+
+int rt_release_cached_contexts(void) {
+    std::lock_guard<std::mutex> lock(g_cache_mu);
+    for (rt_context*& c : g_cache) {
+        rt_context_destroy(c);
+        c = nullptr;
+    }
+    g_cache.clear();
     return RT_OK;
 }
 

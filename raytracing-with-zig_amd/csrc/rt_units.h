@@ -1,0 +1,203 @@
+// rt_units.h — device side of the unit scheduler and the ordered in-kernel accumulation
+// (rt_kernel.h "Work units").  Shared by the parity kernels (rt_kernel.hip) and the
+// fast kernel (rt_kernel_fast.hip).
+//
+// Hand-off between waves (possibly on different XCDs, whose L2s are not coherent with each other):
+// the running sums are stored write-through (sc1: agent-scope relaxed atomic stores), every storing
+// wave drains them (s_waitcnt vmcnt(0)) before ONE lane stores the tile's flag (an sc1 store), and
+// the consumer polls the flag with an sc1 load and reads the sums with sc1 loads only — the
+// MI355X hand-off recipe (cdna_hip_programming.md Guideline 16, R1 with sc1 loads).  A wave's ring
+// is private to it; it is read back with sc1 loads (L2, behind the wave's own vmcnt(0)).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "rt_device.h"
+#include "rt_kernel.h"
+
+namespace rtk {
+
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+typedef __attribute__((address_space(1))) uint32_t gu32;
+
+__device__ __forceinline__ double ld_wt(const double* p) {  // global_load_dwordx2 ... sc1
+    return __builtin_bit_cast(double, __hip_atomic_load((gu64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+__device__ __forceinline__ void st_wt(double* p, double v) {  // global_store_dwordx2 ... sc1
+    __hip_atomic_store((gu64*)p, __builtin_bit_cast(unsigned long long, v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// A wave that cannot claim and has nothing to trace sleeps between polls; a bug that broke the
+// dependency chain would otherwise hang the GPU, so the wait is bounded (≈ 0.5 s of sleeping per
+// wave): past it the wave reports it in ctr[8] and gives up (the host returns RT_ERR_HIP).
+constexpr uint32_t kSpinLimit = 1u << 22;
+
+// Wave-uniform scheduler state (every member is the same in all 64 lanes).
+struct UnitSched {
+    const UnitArgs& ua;
+    double* ring;                    // this wave's ring: kSlots x [kUnitS * 64][3]
+    uint32_t busy = 0;               // slots holding a unit that is not finalised yet
+    uint32_t cur_slot = 0, cur = 0, end = 0;  // the slot being handed out: items [cur, end)
+    uint32_t cur_tile = 0, cur_s0 = 0;
+    uint32_t st_u[kSlots];           // unit id held by each slot
+    uint32_t spins = 0;
+    bool drained = false;            // the claim counter is exhausted
+    bool failed = false;             // spin limit reached (reported in ctr[8])
+
+    __device__ UnitSched(const UnitArgs& a, uint32_t wave) : ua(a), ring(a.ring + (size_t)wave * kRingWaveDoubles) {
+#pragma unroll
+        for (uint32_t j = 0; j < kSlots; ++j) st_u[j] = 0;
+    }
+    __device__ __forceinline__ bool can_claim() const { return !drained && (~busy & kSlotMask) != 0; }
+
+    // Claims the next unit into a free slot and makes it the one handed out; false if there is no
+    // free slot or no unit left.
+    __device__ __forceinline__ bool claim(uint32_t lane) {
+        const uint32_t freem = ~busy & kSlotMask;
+        if (drained || freem == 0) return false;
+        uint32_t u = 0;
+        if (lane == 0) u = (uint32_t)atomicAdd(ua.ctr, 1ull);
+        u = __builtin_amdgcn_readfirstlane(u);
+        if (u >= ua.n_units) {
+            drained = true;
+            return false;
+        }
+        const uint32_t k = fastdiv(u, ua.div_tiles), tile = u - k * ua.n_tiles;
+        uint32_t s0, n;
+        chunk_range(ua, k, &s0, &n);
+        const uint32_t js = (uint32_t)__builtin_ctz(freem);
+#pragma unroll
+        for (uint32_t j = 0; j < kSlots; ++j) st_u[j] = j == js ? u : st_u[j];
+        busy |= 1u << js;
+        cur_slot = js;
+        cur = 0;
+        end = n * 64;
+        cur_tile = tile;
+        cur_s0 = s0;
+        return true;
+    }
+
+    // Hands items to the lanes without a path (wave-uniform loop).  A lane handed item m of the
+    // current unit gets pixel q = 64 * tile + m % 64 and sample s0 + m / 64; items of pixels past
+    // the launch's last (a partial last tile) are skipped.  `fresh` marks lanes that start a path.
+    __device__ __forceinline__ void refill(bool& active, bool& fresh, uint32_t& myslot, uint32_t& mi, uint32_t& q,
+                                           uint32_t& s, uint32_t lane) {
+        uint64_t needy = __ballot(!active);
+        while (needy != 0) {
+            if (cur >= end && !claim(lane)) break;
+            const uint32_t avail = end - cur;
+            const uint32_t want = (uint32_t)__popcll(needy);
+            const uint32_t take = avail < want ? avail : want;
+            if (!active) {
+                const uint32_t rk = __builtin_amdgcn_mbcnt_hi((uint32_t)(needy >> 32),
+                                                              __builtin_amdgcn_mbcnt_lo((uint32_t)needy, 0u));
+                if (rk < take) {
+                    const uint32_t m = cur + rk;
+                    const uint32_t pq = cur_tile * 64 + (m & 63);
+                    if (pq < ua.P) {
+                        myslot = cur_slot;
+                        mi = m;
+                        q = pq;
+                        s = cur_s0 + (m >> 6);
+                        active = true;
+                        fresh = true;
+                    }
+                }
+            }
+            cur += take;
+            needy = __ballot(!active);
+        }
+    }
+
+    // The color of a finished item goes to its unit's ring slot: [slot][m][3].
+    __device__ __forceinline__ void store(uint32_t slot, uint32_t m, double x, double y, double z) const {
+        double* d = ring + (size_t)slot * kRingSlotDoubles + 3 * m;
+        d[0] = x;
+        d[1] = y;
+        d[2] = z;
+    }
+
+    // Finalises ONE unit whose items have all ended (none in flight in any lane), if any: lane l
+    // adds the unit's colors of pixel l, in sample order, to the pixel's running sum
+    // (camera.zig:133-136) after the previous chunk of the same tile; the last chunk scales by
+    // pixelSamplesScale (camera.zig:137) and writes the framebuffer (optionally Color.toRgb,
+    // color.zig:63-80).  Every lane takes part (all 64 are converged here).  One call site and one
+    // unit per call keep a single inlined copy of the body.  Returns whether a unit was finalised.
+    __device__ __forceinline__ bool finalize_one(bool active, uint32_t myslot, uint32_t lane) {
+        if (busy == 0) return false;
+        uint32_t ready = 0;
+#pragma unroll
+        for (uint32_t j = 0; j < kSlots; ++j) {
+            const bool issued = j != cur_slot || cur >= end;
+            if (((busy >> j) & 1u) && issued && __ballot(active && myslot == j) == 0) ready |= 1u << j;
+        }
+        while (ready) {
+            const uint32_t j = (uint32_t)__builtin_ctz(ready);
+            ready &= ready - 1;
+            uint32_t u = st_u[0];
+#pragma unroll
+            for (uint32_t jj = 1; jj < kSlots; ++jj) u = jj == j ? st_u[jj] : u;
+            const uint32_t k = fastdiv(u, ua.div_tiles), tile = u - k * ua.n_tiles;
+            uint32_t f = 0;
+            if (lane == 0) f = __hip_atomic_load((gu32*)ua.flags + tile, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            f = __builtin_amdgcn_readfirstlane(f);
+            if (f != k) continue;  // the previous chunk of this tile is not finalised yet
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keeps the sc1 loads below the poll
+            uint32_t s0, n;
+            chunk_range(ua, k, &s0, &n);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's ring stores have reached L2
+            const uint32_t q = tile * 64 + lane;
+            if (q < ua.P) {
+                double x = 0.0, y = 0.0, z = 0.0;
+                if (k) {
+                    x = ld_wt(ua.sums + 3 * (size_t)q + 0);
+                    y = ld_wt(ua.sums + 3 * (size_t)q + 1);
+                    z = ld_wt(ua.sums + 3 * (size_t)q + 2);
+                }
+                const double* rs = ring + (size_t)j * kRingSlotDoubles + 3 * lane;
+#pragma unroll 1
+                for (uint32_t t = 0; t < n; ++t) {
+                    x = x + ld_wt(rs + 0);
+                    y = y + ld_wt(rs + 1);
+                    z = z + ld_wt(rs + 2);
+                    rs += 3 * 64;
+                }
+                if (k + 1 < ua.n_chunks) {
+                    st_wt(ua.sums + 3 * (size_t)q + 0, x);
+                    st_wt(ua.sums + 3 * (size_t)q + 1, y);
+                    st_wt(ua.sums + 3 * (size_t)q + 2, z);
+                } else if (ua.out_format == 0) {
+                    double* o = (double*)ua.out + 3 * (size_t)q;
+                    o[0] = x * ua.scale;  // avgColor = pixelColor * pixelSamplesScale
+                    o[1] = y * ua.scale;
+                    o[2] = z * ua.scale;
+                } else {
+                    uint8_t* o = (uint8_t*)ua.out + 3 * (size_t)q;
+                    o[0] = to_byte(x * ua.scale);
+                    o[1] = to_byte(y * ua.scale);
+                    o[2] = to_byte(z * ua.scale);
+                }
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains before the flag
+            if (lane == 0 && k + 1 < ua.n_chunks)
+                __hip_atomic_store((gu32*)ua.flags + tile, k + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            busy &= ~(1u << j);
+            return true;
+        }
+        return false;
+    }
+
+    // Nothing to trace in this wave: wait for a dependency (bounded).  False: give up (reported).
+    __device__ __forceinline__ bool wait(uint32_t lane) {
+        if (++spins > kSpinLimit) {
+            if (lane == 0) atomicOr(ua.ctr + 8, 1ull);
+            failed = true;
+            return false;
+        }
+        __builtin_amdgcn_s_sleep(2);
+        return true;
+    }
+};
+
+}  // namespace rtk

@@ -201,6 +201,10 @@ class DeviceRenderer:
                                             C.c_void_p(d_out_ptr), C.c_void_p(d_stats_ptr or 0),
                                             C.c_void_p(stream_ptr or 0)))
 
+    def sync(self):
+        """Waits for the last render; raises if the kernel recorded a failure."""
+        check("rt_context_sync", self.lib.rt_context_sync(self.ctx))
+
     def set_precision(self, precision):
         """"f64" (parity kernel, default) or "f32" (fast mode) for later renders."""
         check("rt_context_set_precision", self.lib.rt_context_set_precision(self.ctx, _PRECISION[precision]))
@@ -297,6 +301,11 @@ def encode_p3(rgb, width, height):
     buf = (C.c_uint8 * size)()
     check("rt_ppm_encode_p3", lib.rt_ppm_encode_p3(ptr, width, height, buf, size))
     return bytes(buf)
+
+
+def release_cached_contexts():
+    """Frees rt_render's per-device cached contexts (the next render creates them again)."""
+    check("rt_release_cached_contexts", load().rt_release_cached_contexts())
 
 
 def sample_key(seed, pixel, sample):

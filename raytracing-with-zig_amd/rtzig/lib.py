@@ -24,6 +24,8 @@ EXPORTED = [
     "rt_context_kernel_times_total",
     "rt_context_enable_profile",
     "rt_context_set_precision",
+    "rt_context_sync",
+    "rt_release_cached_contexts",
     "rt_scene_final",
     "rt_scene_chapter13",
     "rt_camera_build",
@@ -65,6 +67,8 @@ def _declare(lib):
         "rt_context_kernel_times_total": (C.c_int, [vp, P(C.c_double), P(C.c_double), P(C.c_uint32)]),
         "rt_context_enable_profile": (C.c_int, [vp, C.c_int]),
         "rt_context_set_precision": (C.c_int, [vp, C.c_int]),
+        "rt_context_sync": (C.c_int, [vp]),
+        "rt_release_cached_contexts": (C.c_int, []),
         "rt_scene_final": (C.c_int, [C.c_uint64, P(RtSphere), C.c_size_t, P(C.c_size_t),
                                      P(C.c_uint64)]),
         "rt_scene_chapter13": (C.c_int, [P(RtSphere), C.c_size_t, P(C.c_size_t)]),

@@ -36,7 +36,7 @@ def test_library_exports_every_symbol():
 
 def test_abi_version_and_error_string():
     lib = rtzig.load()
-    assert lib.rt_abi_version() == 2
+    assert lib.rt_abi_version() == 3
     assert isinstance(lib.rt_last_error(), bytes)
 
 

@@ -1,0 +1,94 @@
+"""Every BASELINE.json GPU config at its STATED spp (SURVEY §8(d) parity targets), through the C ABI.
+
+* bit-exact against oracle B (the reference arithmetic with the GPU's per-(pixel, sample) streams):
+  config 2 whole image at 100 spp; configs 3 and 4 on 8 interleaved rows at 500 spp; config 5 on one
+  row at 10000 spp (629 sample chunks: the in-kernel ordered accumulation hands each pixel's running
+  sum from unit to unit, camera.zig:133-136);
+* statistical against the reference's OWN images (SURVEY §8(c) ladder 3) for configs 2 and 3, whose
+  seeds are unknown: per-channel image-mean |delta| <= 1.0 (8-bit units) and 8x8 box RMSE <= 1.5x
+  the A-vs-B RMSE (oracle A's sequential stream vs oracle B's per-sample streams, same scene).
+"""
+import os
+
+import numpy as np
+import pytest
+
+import rtzig
+from oracle_lib import read_ppm
+
+pytestmark = pytest.mark.gpu
+
+
+def _box_rmse(a, b):
+    box = lambda x: x[:224].reshape(28, 8, 50, 8, 3).astype(np.float64).mean(axis=(1, 3))
+    return float(np.sqrt(((box(a) - box(b)) ** 2).mean()))
+
+
+def _rows(cam, row0, step, n):
+    import torch
+    r = rtzig.DeviceRenderer(0)
+    r.set_scene(cam.scene.world)
+    r.enable_timing(True)
+    buf = torch.zeros((n, cam.width, 3), dtype=torch.float64, device="cuda:0")
+    stats = torch.zeros(2, dtype=torch.int64, device="cuda:0")
+    r.render_rows_async(cam.cam, buf.data_ptr(), row0=row0, row_step=step, n_rows=n, d_stats_ptr=stats.data_ptr())
+    r.sync()
+    launches = r.kernel_times_total()[2]
+    r.close()
+    return buf.cpu().numpy(), [int(x) for x in stats.cpu().tolist()], launches
+
+
+def test_config2_full_image_100spp_bit_exact(oracle):
+    """Config 2: chapter 9 (two Lambertian spheres), 400x225, 100 spp, depth 50 — every pixel."""
+    cam = rtzig.chapter9_camera(spp=100)
+    st = {}
+    out = rtzig.render(cam.cam, cam.scene.world, n_gpus=1, stats=st)
+    ref, rays = oracle.render_b(cam.cam, cam.scene.world, threads=16)
+    assert np.array_equal(out, ref)
+    assert st["rays"] == rays and st["samples"] == 400 * 225 * 100
+
+
+@pytest.mark.parametrize("config", ["chapter9", "chapter13"])
+def test_configs2_3_statistically_match_reference_images(oracle, golden_dir, config):
+    """Configs 2 and 3 vs the reference's images/chapter9.ppm and images/chapter13.ppm (400x225,
+    100 spp): the GPU's fused-toRgb output against the fixture, with the A-vs-B noise floor."""
+    cam = rtzig.chapter9_camera(spp=100) if config == "chapter9" else rtzig.chapter13_camera(width=400, spp=100)
+    gpu = rtzig.render(cam.cam, cam.scene.world, n_gpus=1, output="rgb8")
+    a, _ = oracle.render_a(cam.cam, cam.scene.world)
+    b, _ = oracle.render_b(cam.cam, cam.scene.world, threads=16)
+    floor = _box_rmse(oracle.to_rgb8(a), oracle.to_rgb8(b))
+    _, _, gold = read_ppm(open(os.path.join(golden_dir, f"{config}.ppm"), "rb").read())
+    assert np.abs(gpu.astype(np.float64).mean(axis=(0, 1)) - gold.astype(np.float64).mean(axis=(0, 1))).max() <= 1.0
+    assert _box_rmse(gpu, gold) <= 1.5 * floor, (_box_rmse(gpu, gold), floor)
+
+
+def test_config3_rows_500spp_bit_exact(oracle):
+    """Config 3: chapter 13 scene + camera, 1200x675, 500 spp — 8 rows spread over the image."""
+    cam = rtzig.chapter13_camera(width=1200, spp=500)
+    assert (cam.width, cam.height) == (1200, 675)
+    out, st, _ = _rows(cam, 3, 83, 8)
+    ref, rays = oracle.render_b(cam.cam, cam.scene.world, row0=3, row_step=83, n_rows=8, threads=16)
+    assert np.array_equal(out, ref)
+    assert st == [rays, 8 * 1200 * 500]
+
+
+def test_config4_rows_500spp_bit_exact(oracle):
+    """Config 4 (the bench workload): final scene, 1200x800, 500 spp — 8 rows spread over the image."""
+    cam = rtzig.final_scene_camera(width=1200, aspect_ratio=1.5, spp=500)
+    assert (cam.width, cam.height, len(cam.scene.world)) == (1200, 800, 485)
+    out, st, _ = _rows(cam, 7, 99, 8)
+    ref, rays = oracle.render_b(cam.cam, cam.scene.world, row0=7, row_step=99, n_rows=8, threads=16)
+    assert np.array_equal(out, ref)
+    assert st == [rays, 8 * 1200 * 500]
+
+
+def test_config5_row_10000spp_bit_exact(oracle):
+    """Config 5: final scene at 3840x2160 (16/9), 10000 spp — one row in one launch (60 tiles x 629
+    sample chunks, every pixel's running sum handed along 628 units)."""
+    cam = rtzig.final_scene_camera(width=3840, aspect_ratio=16 / 9, spp=10000)
+    assert (cam.width, cam.height) == (3840, 2160)
+    out, st, launches = _rows(cam, 1333, 1, 1)
+    assert launches == 1
+    ref, rays = oracle.render_b(cam.cam, cam.scene.world, row0=1333, row_step=1, n_rows=1, threads=16)
+    assert np.array_equal(out, ref)
+    assert st == [rays, 3840 * 10000]

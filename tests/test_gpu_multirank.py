@@ -1,0 +1,79 @@
+"""The multi-rank path through the HIP kernel: 2 and 3 ranks in separate
+processes share GPU 0, each renders its interleaved rows (rows j = rank + k*world) with the
+DeviceRenderer (C ABI -> HIP kernel), and rtzig.dist gathers them to rank 0 over gloo.  The gathered
+image must equal the 1-rank GPU image and oracle B bit for bit: the RNG is keyed by the global pixel,
+so the partition cannot change a bit.  (bench.py runs the same partition over RCCL, one GPU per
+rank.)"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+WIDTH, SPP = 160, 6
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _rank(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch
+    import torch.distributed as dist
+
+    import rtzig
+    from rtzig import dist as rdist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.cuda.set_device(0)
+        cam = rtzig.final_scene_camera(width=WIDTH, aspect_ratio=16 / 9, spp=SPP)
+        H, W = cam.height, cam.width
+        row0, step, n = rdist.rank_rows(H, rank, world)
+        R = rdist.rows_per_rank(H, world)
+        r = rtzig.DeviceRenderer(0)
+        r.set_scene(cam.scene.world)
+        local = torch.zeros((R, W, 3), dtype=torch.float64, device="cuda:0")
+        if n:
+            r.render_rows_async(cam.cam, local.data_ptr(), row0=row0, row_step=step, n_rows=n,
+                                stream_ptr=torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        img = rdist.gather_image(local.cpu(), H, rank, world)  # gloo gathers host tensors
+        r.close()
+        if rank == 0:
+            q.put(img.numpy().copy())
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_hip_ranks_gather_equals_single_rank(oracle, world):
+    import rtzig
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        img = q.get(timeout=100)
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    assert all(p.exitcode == 0 for p in procs)
+    cam = rtzig.final_scene_camera(width=WIDTH, aspect_ratio=16 / 9, spp=SPP)
+    single = rtzig.render(cam.cam, cam.scene.world, n_gpus=1)
+    ref, _ = oracle.render_b(cam.cam, cam.scene.world, threads=16)
+    assert img.shape == single.shape
+    assert np.array_equal(img, single)
+    assert np.array_equal(img, ref)

@@ -2,7 +2,7 @@
 """Msamples/s of the parity kernel on every BASELINE.json GPU config (one MI355X, sample + reduce
 kernels by HIP events, inputs resident).  Config 5 (3840x2160, 10000 spp) runs at a bounded spp
 (--stress-spp) so the run stays short; the rate is per sample, and at 10000 spp only the number
-of sample-chunk launches grows (the workspace holds up to 64 GiB of per-sample colors).
+of units grows with spp (one launch per frame, in-kernel ordered accumulation).
 
     python tools/configs_bench.py [--stress-spp 200] [--out profiles/r01_configs.json]
 """

@@ -1,0 +1,104 @@
+#!/usr/bin/env python3
+"""Summarise a tools/profile.sh run (gpurun_out/prof_<tag>/) into profiles/<tag>/ and
+profiles/pmc_traffic.json (read by bench.py: roofline.traffic, roofline.issue).
+
+    python tools/pmc_summary.py <tag> [workload]
+
+The PMC passes run `bench.py --steps 1 --warmup 0`: ONE timed frame, possibly several sample-kernel
+launches (sample chunks); every counter is summed over the timed kernel's dispatches = per frame.
+(The instrumented frame runs the kProf = true instantiation and is excluded by name.)
+
+Units (MI355X_MICROARCH.md): FETCH_SIZE / WRITE_SIZE in KiB; SQ_WAVE_CYCLES, SQ_WAIT_*,
+SQ_ACTIVE_INST_* and SQ_BUSY_CYCLES count quad-cycles; SQ_INSTS_* count wave-instructions; the
+effective clock is GRBM_GUI_ACTIVE / 8 XCDs / the kernel's wall time.
+VALU issue model (the guide: a wave64 VALU instruction issues over 2 cycles on a SIMD-32; f64
+add/mul/fma at half rate, 4 cycles; transcendentals 8):
+    issue cycles = 2 * n_32bit + 4 * n_f64 + 8 * n_trans,   frac = issue / (1024 SIMDs x clock x t)
+"""
+import csv
+import glob
+import json
+import os
+import shutil
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SIMDS = 1024
+
+
+def timed(name):
+    return "sample_kernel" in name and not name.split("(")[0].endswith("true>")
+
+
+def main(tag, workload):
+    src = os.path.join(ROOT, "gpurun_out", f"prof_{tag}")
+    dst = os.path.join(ROOT, "profiles", tag)
+    os.makedirs(dst, exist_ok=True)
+    out = {"tag": tag, "workload": workload}
+    st = os.path.join(src, "trace", "trace_kernel_stats.csv")
+    if os.path.exists(st):
+        shutil.copy(st, os.path.join(dst, "kernel_stats.csv"))
+        for r in csv.DictReader(open(st)):
+            if timed(r["Name"]):
+                out["trace"] = {"kernel": r["Name"], "calls": int(r["Calls"]), "avg_ms": float(r["AverageNs"]) / 1e6,
+                                "total_ms": float(r["TotalDurationNs"]) / 1e6, "percent": float(r["Percentage"])}
+    tb = os.path.join(src, "trace_bench.json")
+    if os.path.exists(tb):
+        shutil.copy(tb, os.path.join(dst, "trace_bench.json"))
+    sums, dur, disp = {}, {}, {}
+    for f in sorted(glob.glob(os.path.join(src, "pmc_*", "pmc_counter_collection.csv"))):
+        rows = [r for r in csv.DictReader(open(f)) if timed(r["Kernel_Name"])]
+        if rows:
+            shutil.copy(f, os.path.join(dst, os.path.basename(os.path.dirname(f)) + ".csv"))
+        for r in rows:
+            c = r["Counter_Name"]
+            sums[c] = sums.get(c, 0.0) + float(r["Counter_Value"])
+            disp.setdefault(c, set()).add(r["Dispatch_Id"])
+            key = (c, r["Dispatch_Id"])
+            dur[key] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9
+            out["vgpr"], out["sgpr"] = int(r["VGPR_Count"]), int(r["SGPR_Count"])
+    kt = lambda c: sum(v for (cc, _), v in dur.items() if cc == c)  # kernel seconds under counter c's pass
+    g = lambda c: sums.get(c, float("nan"))
+    out["launches_per_frame"] = len(disp.get("SQ_WAVES", disp.get("FETCH_SIZE", ())))
+    out["counters_per_frame"] = sums
+    if "FETCH_SIZE" in sums and "WRITE_SIZE" in sums:
+        out["hbm_bytes_per_frame"] = (sums["FETCH_SIZE"] + sums["WRITE_SIZE"]) * 1024
+        out["fetch_bytes_per_frame"] = sums["FETCH_SIZE"] * 1024
+        out["write_bytes_per_frame"] = sums["WRITE_SIZE"] * 1024
+    if "GRBM_GUI_ACTIVE" in sums:
+        T = kt("GRBM_GUI_ACTIVE")
+        clock = g("GRBM_GUI_ACTIVE") / 8 / T
+        out["kernel_s_pmc_pass"] = T
+        out["clock_GHz"] = clock / 1e9
+        if "SQ_INSTS_VALU_ADD_F64" in sums and "SQ_INSTS_VALU" in sums:
+            n64 = g("SQ_INSTS_VALU_ADD_F64") + g("SQ_INSTS_VALU_MUL_F64") + g("SQ_INSTS_VALU_FMA_F64")
+            ntr = g("SQ_INSTS_VALU_TRANS_F32") + g("SQ_INSTS_VALU_TRANS_F64")
+            n32 = g("SQ_INSTS_VALU") - n64 - ntr
+            cyc = 2 * n32 + 4 * n64 + 8 * ntr
+            out["valu_issue_cycles_per_frame"] = cyc
+            out["valu_issue_frac_pmc_pass"] = cyc / (SIMDS * clock * T)
+            out["valu_insts"] = {"total": g("SQ_INSTS_VALU"), "f64": n64, "trans": ntr, "other_32bit": n32}
+        if "SQ_WAVE_CYCLES" in sums and "SQ_ACTIVE_INST_ANY" in sums:
+            wc = g("SQ_WAVE_CYCLES")
+            out["wave_cycle_split"] = {"active_inst_any": g("SQ_ACTIVE_INST_ANY") / wc,
+                                       "wait_inst_any (issue stall)": g("SQ_WAIT_INST_ANY") / wc,
+                                       "wait_inst_lds (part of issue stall)": g("SQ_WAIT_INST_LDS") / wc,
+                                       "wait_any (parked on s_waitcnt)": g("SQ_WAIT_ANY") / wc}
+            out["waves_per_simd_avg"] = 4 * wc / (SIMDS * clock * T)
+        if "SQ_THREAD_CYCLES_VALU" in sums:
+            out["valu_lanes_active_of_64"] = g("SQ_THREAD_CYCLES_VALU") / g("SQ_ACTIVE_INST_VALU")
+        if "SQ_LDS_IDX_ACTIVE" in sums:
+            out["lds"] = {"active_frac_of_cu_cycles": g("SQ_LDS_IDX_ACTIVE") / (256 * clock * T),
+                          "bank_conflict_frac_of_active": g("SQ_LDS_BANK_CONFLICT") / g("SQ_LDS_IDX_ACTIVE")}
+    json.dump(out, open(os.path.join(dst, "summary.json"), "w"), indent=1)
+    if "hbm_bytes_per_frame" in out:
+        keep = {k: out[k] for k in ("workload", "tag", "launches_per_frame", "hbm_bytes_per_frame", "fetch_bytes_per_frame",
+                                    "write_bytes_per_frame", "valu_issue_cycles_per_frame", "clock_GHz") if k in out}
+        keep["source"] = (f"profiles/{tag}/summary.json (rocprofv3 --pmc, separate passes; FETCH_SIZE + WRITE_SIZE "
+                          "KiB x 1024, summed over the frame's sample-kernel launches)")
+        json.dump(keep, open(os.path.join(ROOT, "profiles", "pmc_traffic.json"), "w"), indent=1)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else "final-render 1200x800 500spp depth50 (485 spheres)")
