@@ -31,8 +31,14 @@ constexpr uint32_t kMaxLdsSpheres = 2048;  // 64 KiB of LDS geometry; above this
 // frame drains): R = spp - n_main * kUnitS in [kUnitS, 2 kUnitS) (or spp if smaller), tail chunk t
 // covers [R - rem(t), R - rem(t + 1)) with rem(t) = ceil(R / 2^t), rem(T + 1) = 0, 2^T >= R.
 // ------------------------------------------------------------------------------------------------
-constexpr uint32_t kUnitS = 16;   // samples per unit of the main chunks
-constexpr uint32_t kSlots = 4;    // units a wave holds at once
+#ifndef RTZIG_UNIT_S
+#define RTZIG_UNIT_S 16
+#endif
+#ifndef RTZIG_SLOTS
+#define RTZIG_SLOTS 4
+#endif
+constexpr uint32_t kUnitS = RTZIG_UNIT_S;  // samples per unit of the main chunks
+constexpr uint32_t kSlots = RTZIG_SLOTS;   // units a wave holds at once
 constexpr uint32_t kSlotMask = (1u << kSlots) - 1;
 constexpr uint32_t kRingSlotDoubles = kUnitS * 64 * 3;
 constexpr uint32_t kRingWaveDoubles = kSlots * kRingSlotDoubles;  // 96 KiB of f64 per wave
@@ -155,7 +161,7 @@ struct BvhArgs {
     uint32_t stack_depth;  // per-lane stack entries the tree needs: its depth (root = 1), <= kMaxDepthBvh
     // The f32 box padding covers ray origins with max|o_i| <= the builder's origin bound; this is
     // that bound rounded down to f32.  A lane whose f32 origin lies beyond it (a secondary ray
-    // leaving an unboundable always-list sphere far out) takes no box culling: it visits every leaf.
+    // leaving an unboundable always-list sphere far out) skips the tree and walks the whole list.
     float origin_bound;
     uint32_t pad;
 };

@@ -317,6 +317,8 @@ struct BvhWalker {
     uint32_t n_always;
     int32_t* stack;                      // LDS, element i of this lane at stack[i * kBlockBvh]
     float origin_bound;                  // BvhArgs::origin_bound
+    const GeoRec* __restrict__ geo_all;  // the whole list in original order (far-origin lanes)
+    uint32_t n_pad;
 
     // always-list sphere q: geometry + original index from global memory (uniform address,
     // read-only data: scalar loads; the compiler emits per-lane vector loads, since it cannot prove
@@ -437,11 +439,23 @@ struct BvhWalker {
         // overflowed plane is +-inf in ray order, and NaN arises only from a NaN origin, which
         // v_max3/v_min3 drop (the box is kept: permissive, never a wrong cull).
         const uint32_t ax = ix < 0 ? 8u : 0u, ay = 16u + (iy < 0 ? 8u : 0u), az = 32u + (iz < 0 ? 8u : 0u);
-        // lanes whose origin lies outside the box padding's origin bound (rt_bvh.cpp) cull nothing:
-        // their box tests are forced to "hit" on the scalar unit (a NaN origin fails every sphere
-        // test anyway; the max drops it)
-        const uint64_t far_mask = __ballot(__builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(ox), __builtin_fabsf(oy)),
-                                                           __builtin_fabsf(oz)) > origin_bound);
+        // A lane whose origin lies outside the box padding's origin bound (rt_bvh.cpp) must not be
+        // culled by the f32 boxes: it walks the whole list linearly instead (the reference's own
+        // scan, exact) and skips the tree.  Only rays leaving an unboundable always-list sphere get
+        // there, so the common path pays one compare and one ballot per ray.  (A NaN origin fails
+        // every sphere test anyway; the max drops it.)
+        const bool far = __builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(ox), __builtin_fabsf(oy)), __builtin_fabsf(oz)) >
+                         origin_bound;
+        if (__builtin_expect(__ballot(far) != 0, 0)) {
+            if (far) {
+                double t;
+                const int k = world_hit<1>(geo_all, n_pad, r, t_min, t_max, &t);
+                pr.tests(n_pad);
+                found = k >= 0;
+                best = found ? (uint32_t)k : 0u;
+                closest = t;
+            }
+        }
         // per-axis constants live in the low half of a register pair; pk_fma_lo broadcasts them to
         // both lanes of the packed fma (op_sel_hi), so they are not duplicated with v_mov
         f2 inv_x, inv_y, inv_z, noi_x, noi_y, noi_z;
@@ -455,7 +469,7 @@ struct BvhWalker {
         // stack: entry 0 holds kDone (written once per lane at kernel start), entries 1..sp the
         // pushed far children; a pop reads entry sp, so popping the empty stack yields kDone
         int32_t* top = stack;  // this lane's stack entry sp (entry i at stack[i * kBlockBvh])
-        int32_t cur = 0;  // root
+        int32_t cur = far ? kDone : 0;  // root
         // while-while (Aila & Laine 2009): every lane advances through internal nodes until it
         // holds a leaf (or is done); then the lanes with a leaf test its spheres together, so the
         // f64 leaf work runs with most lanes active instead of whenever any one lane hits a leaf.
@@ -502,8 +516,7 @@ struct BvhWalker {
                 // The three compares are taken as wave masks and combined on the scalar unit, and
                 // the selects are v_cndmask on those masks: 3 compares + 5 selects (the compiler's
                 // form of the same logic re-compared a negated mask on the VALU).
-                const uint64_t m0 = __ballot(n0 <= f0) | far_mask, m1 = __ballot(n1 <= f1) | far_mask,
-                               mf = __ballot(n0 <= n1);
+                const uint64_t m0 = __ballot(n0 <= f0), m1 = __ballot(n1 <= f1), mf = __ballot(n0 <= n1);
                 const uint64_t pick0 = m0 & (~m1 | mf);  // both: nearer; one: that one
                 const uint64_t any = m0 | m1, both = m0 & m1;
                 const int32_t near = sel_mask(ref1, ref0, pick0), far = sel_mask(ref0, ref1, pick0);
@@ -625,8 +638,8 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
     while (true) {
         uint64_t t_top = 0;
         if constexpr (kProf) t_top = __builtin_amdgcn_s_memtime();
-        // ---- finalise a unit whose samples have all ended (rt_units.h) ---------------------------
-        const bool progressed = us.finalize_one(active, myslot, lane);
+        // ---- finalise one unit whose samples have all ended (rt_units.h) --------------------------
+        const bool progressed = us.finalize_one(us.ready_mask(active, myslot), lane);
         // ---- hand new items to lanes without a path (wave-uniform control flow) ----------------
         bool fresh = false;
         uint32_t fq = 0, fs = 0;  // pixel (launch-local) and sample of a freshly handed item
@@ -647,10 +660,12 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
             att = mk(1, 1, 1);
             bounce = 0;
         }
-        if (__ballot(active) == 0) {
-            // nothing to trace: finish, or claim again next iteration, or wait for the previous chunk
-            // of a tile another wave holds
+        const bool idle = __ballot(active) == 0;
+        if (idle) {
+            // nothing to trace: finish (no unit left, none held), or claim again next iteration
             if (us.busy == 0 && us.drained) break;
+            // a wave that can neither finalise nor claim waits for the previous chunk of a tile
+            // another wave holds
             if (!progressed && !us.can_claim() && !us.wait(lane)) break;
             // else: the rest of the iteration runs with every lane idle (no back edge of its own:
             // one measured 17 extra VGPRs)
@@ -918,7 +933,7 @@ __global__ __launch_bounds__(kBlockBvh) void sample_kernel_bvh(KernelParams p, B
         leaves = ll;
     }
     path_loop<kProf>(p, BvhWalker<kLdsScene>{nodes, leaves, b.always_geo, b.always_sid, b.n_always, stack + threadIdx.x,
-                                              b.origin_bound}, geo_g,
+                                              b.origin_bound, geo_g, p.n_pad}, geo_g,
                      mat_g, ua, stats);
 }
 

@@ -327,7 +327,8 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
     uint64_t rays = 0, nsamples = 0;
 
     while (true) {
-        const bool progressed = us.finalize_one(active, myslot, lane);
+        // ---- finalise one unit whose samples have all ended (rt_units.h) --------------------------
+        const bool progressed = us.finalize_one(us.ready_mask(active, myslot), lane);
         // ---- refill (as the parity kernel's path_loop) -----------------------------------------
         bool fresh = false;
         uint32_t fq = 0, fs = 0;
@@ -343,8 +344,11 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
             att = mk(1, 1, 1);
             bounce = 0;
         }
-        if (__ballot(active) == 0) {
+        const bool idle = __ballot(active) == 0;
+        if (idle) {
             if (us.busy == 0 && us.drained) break;
+            // a wave that can neither finalise nor claim waits for the previous chunk of a tile
+            // another wave holds
             if (!progressed && !us.can_claim() && !us.wait(lane)) break;
             // else: the rest of the iteration runs with every lane idle (no back edge of its own:
             // one measured 17 extra VGPRs)

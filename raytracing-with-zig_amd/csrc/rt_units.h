@@ -7,7 +7,8 @@
 // wave drains them (s_waitcnt vmcnt(0)) before ONE lane stores the tile's flag (an sc1 store), and
 // the consumer polls the flag with an sc1 load and reads the sums with sc1 loads only — the
 // MI355X hand-off recipe (cdna_hip_programming.md Guideline 16, R1 with sc1 loads).  A wave's ring
-// is private to it; it is read back with sc1 loads (L2, behind the wave's own vmcnt(0)).
+// is private to it and written and read by its own CU: plain stores, plain loads behind the wave's
+// own s_waitcnt vmcnt(0) (a workgroup's L1 sees its own CU's stores).
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -32,6 +33,7 @@ __device__ __forceinline__ void st_wt(double* p, double v) {  // global_store_dw
 // dependency chain would otherwise hang the GPU, so the wait is bounded (≈ 0.5 s of sleeping per
 // wave): past it the wave reports it in ctr[8] and gives up (the host returns RT_ERR_HIP).
 constexpr uint32_t kSpinLimit = 1u << 22;
+
 
 // Wave-uniform scheduler state (every member is the same in all 64 lanes).
 struct UnitSched {
@@ -118,20 +120,20 @@ struct UnitSched {
         d[2] = z;
     }
 
-    // Finalises ONE unit whose items have all ended (none in flight in any lane), if any: lane l
-    // adds the unit's colors of pixel l, in sample order, to the pixel's running sum
-    // (camera.zig:133-136) after the previous chunk of the same tile; the last chunk scales by
-    // pixelSamplesScale (camera.zig:137) and writes the framebuffer (optionally Color.toRgb,
-    // color.zig:63-80).  Every lane takes part (all 64 are converged here).  One call site and one
-    // unit per call keep a single inlined copy of the body.  Returns whether a unit was finalised.
-    __device__ __forceinline__ bool finalize_one(bool active, uint32_t myslot, uint32_t lane) {
-        if (busy == 0) return false;
+    // Slots whose unit has been handed out completely and has no item in flight in any lane.
+    __device__ __forceinline__ uint32_t ready_mask(bool active, uint32_t myslot) const {
         uint32_t ready = 0;
 #pragma unroll
         for (uint32_t j = 0; j < kSlots; ++j) {
             const bool issued = j != cur_slot || cur >= end;
             if (((busy >> j) & 1u) && issued && __ballot(active && myslot == j) == 0) ready |= 1u << j;
         }
+        return ready;
+    }
+
+    __device__ __forceinline__ bool finalize_one(uint32_t ready, uint32_t lane) {
+        if (ready == 0) return false;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's ring stores have completed
         while (ready) {
             const uint32_t j = (uint32_t)__builtin_ctz(ready);
             ready &= ready - 1;
@@ -139,14 +141,15 @@ struct UnitSched {
 #pragma unroll
             for (uint32_t jj = 1; jj < kSlots; ++jj) u = jj == j ? st_u[jj] : u;
             const uint32_t k = fastdiv(u, ua.div_tiles), tile = u - k * ua.n_tiles;
-            uint32_t f = 0;
-            if (lane == 0) f = __hip_atomic_load((gu32*)ua.flags + tile, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            f = __builtin_amdgcn_readfirstlane(f);
+            uint32_t f = k;
+            if (k) {  // chunk 0 has no predecessor
+                if (lane == 0) f = __hip_atomic_load((gu32*)ua.flags + tile, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                f = __builtin_amdgcn_readfirstlane(f);
+            }
             if (f != k) continue;  // the previous chunk of this tile is not finalised yet
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keeps the sc1 loads below the poll
             uint32_t s0, n;
             chunk_range(ua, k, &s0, &n);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's ring stores have reached L2
             const uint32_t q = tile * 64 + lane;
             if (q < ua.P) {
                 double x = 0.0, y = 0.0, z = 0.0;
@@ -155,12 +158,13 @@ struct UnitSched {
                     y = ld_wt(ua.sums + 3 * (size_t)q + 1);
                     z = ld_wt(ua.sums + 3 * (size_t)q + 2);
                 }
+                // the ring is this wave's own, written by this CU: plain loads behind the drain
                 const double* rs = ring + (size_t)j * kRingSlotDoubles + 3 * lane;
-#pragma unroll 1
+#pragma unroll 8
                 for (uint32_t t = 0; t < n; ++t) {
-                    x = x + ld_wt(rs + 0);
-                    y = y + ld_wt(rs + 1);
-                    z = z + ld_wt(rs + 2);
+                    x = x + rs[0];
+                    y = y + rs[1];
+                    z = z + rs[2];
                     rs += 3 * 64;
                 }
                 if (k + 1 < ua.n_chunks) {

@@ -12,6 +12,7 @@ import json
 import os
 import statistics
 import sys
+import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "raytracing-with-zig_amd"))
@@ -67,14 +68,18 @@ for spec in args.libs:  # "lib.so" or "lib.so:VAR=VAL" (an environment variable 
     runs.append((spec, L, ctx))
 times = {p: [] for p, _, _ in runs}
 rtimes = {p: [] for p, _, _ in runs}
+wtimes = {p: [] for p, _, _ in runs}  # wall time of render + synchronize (sample + reduce kernels of older builds)
 ref = None
 for rnd in range(args.rounds + 1):
     for path, L, ctx in runs:
         if envs[path]:
             os.environ[envs[path][0]] = envs[path][1]
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
         rc = L.rt_render_rows_async(ctx, C.byref(cam.cam), 0, 0, args.row_step, NR, C.c_void_p(out.data_ptr()), None, None)
         assert rc == 0, L.rt_last_error()
         torch.cuda.synchronize()
+        tw = (time.perf_counter() - t0) * 1e3
         if envs[path]:
             del os.environ[envs[path][0]]
         a, b = C.c_double(), C.c_double()
@@ -87,7 +92,9 @@ for rnd in range(args.rounds + 1):
         if rnd > 0:
             times[path].append(a.value)
             rtimes[path].append(b.value)
+            wtimes[path].append(tw)
 res = {p: {"median_ms": round(statistics.median(t), 3), "min_ms": round(min(t), 3),
            "Msamples_s": round(W * NR * args.spp / statistics.median(t) / 1e3, 1),
-           "reduce_median_ms": round(statistics.median(rtimes[p]), 4)} for p, t in times.items()}
+           "reduce_median_ms": round(statistics.median(rtimes[p]), 4),
+           "wall_median_ms": round(statistics.median(wtimes[p]), 3)} for p, t in times.items()}
 print(json.dumps({"config": f"{args.scene} {W}x{H} {args.spp}spp rows 0::{args.row_step}", "results": res}))
