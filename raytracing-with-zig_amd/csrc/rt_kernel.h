@@ -27,18 +27,10 @@ constexpr uint32_t kMaxLdsSpheres = 2048;  // 64 KiB of LDS geometry; above this
 // chunk of the same tile has been finalised (per-tile flag) — and writes the sum back (write-through
 // sc1 stores, drained, then the flag: MI355X hand-off recipe, any XCD), or, for the last chunk,
 // writes the framebuffer (scale + optional Color.toRgb).  No per-sample buffer and no reduce pass.
-// Chunks: kUnitS samples each, then a halving tail down to 1 sample (fine-grained units while the
-// frame drains): R = spp - n_main * kUnitS in [kUnitS, 2 kUnitS) (or spp if smaller), tail chunk t
-// covers [R - rem(t), R - rem(t + 1)) with rem(t) = ceil(R / 2^t), rem(T + 1) = 0, 2^T >= R.
+// Chunks: kUnitS samples each, shrinking towards the end of the launch (rt_schedule.hpp).
 // ------------------------------------------------------------------------------------------------
-#ifndef RTZIG_UNIT_S
-#define RTZIG_UNIT_S 16
-#endif
-#ifndef RTZIG_SLOTS
-#define RTZIG_SLOTS 4
-#endif
-constexpr uint32_t kUnitS = RTZIG_UNIT_S;  // samples per unit of the main chunks
-constexpr uint32_t kSlots = RTZIG_SLOTS;   // units a wave holds at once
+constexpr uint32_t kUnitS = 16;  // samples per unit of the main chunks (ring slot size)
+constexpr uint32_t kSlots = 4;   // units a wave holds at once (3 measured equal; 2, 6, 8 slower)
 constexpr uint32_t kSlotMask = (1u << kSlots) - 1;
 constexpr uint32_t kRingSlotDoubles = kUnitS * 64 * 3;
 constexpr uint32_t kRingWaveDoubles = kSlots * kRingSlotDoubles;  // 96 KiB of f64 per wave
@@ -51,26 +43,19 @@ struct UnitArgs {
     void* out;                 // [P][3] f64 linear or u8 RGB (the last chunk's finalisation)
     unsigned long long* ctr;   // kCtrBytes: [0] claim counter, [8] error word
     FastDiv div_tiles;         // u -> (chunk, tile)
+    const uint32_t* chunk_s0;  // [n_chunks + 1]: chunk k covers samples [chunk_s0[k], chunk_s0[k + 1])
     uint32_t n_tiles, n_units; // n_units = n_tiles * n_chunks < 2^32
-    uint32_t n_main, tail_r;   // main chunks of kUnitS samples; tail length R
-    uint32_t tail_t, n_chunks; // 2^tail_t >= R; n_chunks = n_main + tail_t + 1
+    uint32_t n_chunks, pad0;
     uint32_t P, out_format;    // pixels of the launch; 0 linear f64, 1 rgb8
     uint32_t ring_waves, pad;  // ring capacity in waves (the launch never has more)
     double scale;              // pixelSamplesScale
 };
 
-// samples [*s0, *s0 + *n) of chunk k
-__host__ __device__ inline void chunk_range(const UnitArgs& u, uint32_t k, uint32_t* s0, uint32_t* n) {
-    if (k < u.n_main) {
-        *s0 = k * kUnitS;
-        *n = kUnitS;
-        return;
-    }
-    const uint32_t t = k - u.n_main, R = u.tail_r;
-    const uint32_t rem = (R + (1u << t) - 1) >> t;
-    const uint32_t rem1 = t < u.tail_t ? (R + (2u << t) - 1) >> (t + 1) : 0u;
-    *s0 = u.n_main * kUnitS + (R - rem);
-    *n = rem - rem1;
+// samples [*s0, *s0 + *n) of chunk k (the table is read-only: scalar loads)
+__device__ __forceinline__ void chunk_range(const UnitArgs& u, uint32_t k, uint32_t* s0, uint32_t* n) {
+    const uint32_t a = u.chunk_s0[k], b = u.chunk_s0[k + 1];
+    *s0 = a;
+    *n = b - a;
 }
 
 constexpr uint32_t kPad = 4;               // sphere list padded to a multiple of this (sentinels)

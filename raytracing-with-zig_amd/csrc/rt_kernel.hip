@@ -887,6 +887,9 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
                 atomicAdd(&stats[5], (unsigned long long)cyc_walk);
                 atomicAdd(&stats[6], (unsigned long long)cyc_shade);
                 atomicAdd(&stats[16], (unsigned long long)cyc_trips);
+                atomicAdd(&stats[17], (unsigned long long)us.spins);       // idle-wave sleeps
+                atomicAdd(&stats[18], (unsigned long long)us.n_dep_wait);  // deferred finalisations
+                atomicAdd(&stats[19], (unsigned long long)us.n_no_slot);   // refills without a free slot
             }
         }
     }

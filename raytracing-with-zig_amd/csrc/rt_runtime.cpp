@@ -31,6 +31,7 @@
 #include "rt_bvh.hpp"
 #include "rt_device.h"
 #include "rt_kernel.h"
+#include "rt_schedule.hpp"
 
 void rt_set_last_error(const std::string& msg);
 
@@ -71,6 +72,10 @@ struct rt_context {
     size_t sums_bytes = 0;
     uint32_t* d_flags = nullptr;
     size_t flags_bytes = 0;
+    std::vector<uint32_t> sched;    // chunk table of the last launch (rt_schedule.hpp), and its copy
+    uint32_t* d_sched = nullptr;
+    size_t sched_bytes = 0;
+    uint64_t sched_lanes = 0;       // resident lanes the schedule is sized for (CUs x 16 waves x 64)
     unsigned long long* d_ctr = nullptr;  // rtk::kCtrBytes, zeroed per launch ([8]: error word)
     const char* last_kernel = "sample_kernel";
     SceneData scene;                // host copy (BVH rebuilds for far-away cameras, scene comparisons)
@@ -340,14 +345,18 @@ bool use_bvh(const rt_context* ctx) {
     return ctx->scene.bvh_ok;
 }
 
-// The chunk schedule of rt_kernel.h "Work units" for `spp` samples.
-void unit_schedule(uint32_t spp, rtk::UnitArgs& ua) {
-    ua.n_main = spp > rtk::kUnitS ? (spp - rtk::kUnitS) / rtk::kUnitS : 0;
-    ua.tail_r = spp - ua.n_main * rtk::kUnitS;
-    uint32_t t = 0;
-    while ((1u << t) < ua.tail_r) ++t;
-    ua.tail_t = t;
-    ua.n_chunks = ua.n_main + t + 1;
+// Uploads the chunk table of rt_schedule.hpp for `spp` samples over `pixels` (unchanged tables are
+// not re-sent; a changed one waits for the last render, which may still read the old one).
+int upload_schedule(rt_context* ctx, uint32_t spp, uint64_t pixels) {
+    std::vector<uint32_t> t = rtk::chunk_schedule(spp, pixels, ctx->sched_lanes, rtk::kUnitS);
+    if (ctx->d_sched && t == ctx->sched) return RT_OK;
+    int rc = quiesce(ctx);
+    if (!rc) rc = ensure_buffer(ctx, (void**)&ctx->d_sched, &ctx->sched_bytes, t.size() * sizeof(uint32_t));
+    if (rc) return rc;
+    HIP_CHECK(hipMemcpyAsync(ctx->d_sched, t.data(), t.size() * sizeof(uint32_t), hipMemcpyHostToDevice, ctx->stream));
+    HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    ctx->sched = std::move(t);
+    return RT_OK;
 }
 
 rtk::KernelParams make_params(const rt_camera* c, uint32_t row0, uint32_t row_step, uint32_t n_rows,
@@ -421,6 +430,7 @@ int rt_context_create(int device, rt_context** out_ctx) {
     int cus = 0;
     if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
     ctx->ring_waves = (uint32_t)std::max(cus, 1) * kMaxWavesPerCU;
+    ctx->sched_lanes = (uint64_t)std::max(cus, 1) * 16 * 64;
     if (e != hipSuccess) {
         const int rc = hip_fail(e, "rt_context_create: stream / event");
         rt_context_destroy(ctx);
@@ -436,7 +446,7 @@ int rt_context_destroy(rt_context* ctx) {
     if (ctx->done_valid) (void)hipEventSynchronize(ctx->done);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     for (void* p : {(void*)ctx->d_geo, (void*)ctx->d_mat, (void*)ctx->d_ring, (void*)ctx->d_sums, (void*)ctx->d_flags,
-                    (void*)ctx->d_ctr, (void*)ctx->d_nodes, (void*)ctx->d_leaves, (void*)ctx->d_always_geo,
+                    (void*)ctx->d_sched, (void*)ctx->d_ctr, (void*)ctx->d_nodes, (void*)ctx->d_leaves, (void*)ctx->d_always_geo,
                     (void*)ctx->d_always_sid, ctx->d_out, (void*)ctx->d_stats})
         (void)hipFree(p);
     if (ctx->h_out) (void)hipHostFree(ctx->h_out);
@@ -506,8 +516,11 @@ int rt_render_rows_async(rt_context* ctx, const rt_camera* cam, uint32_t output_
     const uint64_t P = (uint64_t)n_rows * cam->image_width;
     rtk::UnitArgs ua;
     std::memset(&ua, 0, sizeof ua);
-    unit_schedule(cam->samples_per_pixel, ua);
     const uint64_t n_tiles = (P + 63) / 64;
+    rc = upload_schedule(ctx, cam->samples_per_pixel, P);
+    if (rc) return rc;
+    ua.chunk_s0 = ctx->d_sched;
+    ua.n_chunks = (uint32_t)(ctx->sched.size() - 1);
     if (n_tiles * ua.n_chunks >= (1ull << 32)) {
         rt_set_last_error("too many work units (rows x samples): render fewer rows per call");
         return RT_ERR_CAPACITY;

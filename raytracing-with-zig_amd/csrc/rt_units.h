@@ -44,6 +44,8 @@ struct UnitSched {
     uint32_t cur_tile = 0, cur_s0 = 0;
     uint32_t st_u[kSlots];           // unit id held by each slot
     uint32_t spins = 0;
+    uint32_t n_dep_wait = 0;   // diagnostics (instrumented build): finalisations deferred on a flag
+    uint32_t n_no_slot = 0;    // ... refills stopped for want of a free slot
     bool drained = false;            // the claim counter is exhausted
     bool failed = false;             // spin limit reached (reported in ctr[8])
 
@@ -57,7 +59,11 @@ struct UnitSched {
     // free slot or no unit left.
     __device__ __forceinline__ bool claim(uint32_t lane) {
         const uint32_t freem = ~busy & kSlotMask;
-        if (drained || freem == 0) return false;
+        if (drained) return false;
+        if (freem == 0) {
+            ++n_no_slot;
+            return false;
+        }
         uint32_t u = 0;
         if (lane == 0) u = (uint32_t)atomicAdd(ua.ctr, 1ull);
         u = __builtin_amdgcn_readfirstlane(u);
@@ -146,7 +152,10 @@ struct UnitSched {
                 if (lane == 0) f = __hip_atomic_load((gu32*)ua.flags + tile, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 f = __builtin_amdgcn_readfirstlane(f);
             }
-            if (f != k) continue;  // the previous chunk of this tile is not finalised yet
+            if (f != k) {  // the previous chunk of this tile is not finalised yet
+                ++n_dep_wait;
+                continue;
+            }
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keeps the sc1 loads below the poll
             uint32_t s0, n;
             chunk_range(ua, k, &s0, &n);

@@ -34,8 +34,9 @@ def gather_image(local, height, rank, world, group=None):
     if world == 1:
         return local[:height]
     if rank == 0:
-        bufs = [torch.empty_like(local) for _ in range(world)]
-        dist.gather(local, gather_list=bufs, dst=0, group=group)
-        return assemble(torch.stack(bufs), height)
+        # the peers' rows land in views of ONE (world, R, W, C) buffer: no stack copy
+        buf = torch.empty((world,) + tuple(local.shape), dtype=local.dtype, device=local.device)
+        dist.gather(local, gather_list=list(buf.unbind(0)), dst=0, group=group)
+        return assemble(buf, height)
     dist.gather(local, dst=0, group=group)
     return None

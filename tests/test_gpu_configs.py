@@ -2,7 +2,7 @@
 
 * bit-exact against oracle B (the reference arithmetic with the GPU's per-(pixel, sample) streams):
   config 2 whole image at 100 spp; configs 3 and 4 on 8 interleaved rows at 500 spp; config 5 on one
-  row at 10000 spp (629 sample chunks: the in-kernel ordered accumulation hands each pixel's running
+  row at 10000 spp (2439 sample chunks: the in-kernel ordered accumulation hands each pixel's running
   sum from unit to unit, camera.zig:133-136);
 * statistical against the reference's OWN images (SURVEY §8(c) ladder 3) for configs 2 and 3, whose
   seeds are unknown: per-channel image-mean |delta| <= 1.0 (8-bit units) and 8x8 box RMSE <= 1.5x
@@ -83,8 +83,8 @@ def test_config4_rows_500spp_bit_exact(oracle):
 
 
 def test_config5_row_10000spp_bit_exact(oracle):
-    """Config 5: final scene at 3840x2160 (16/9), 10000 spp — one row in one launch (60 tiles x 629
-    sample chunks, every pixel's running sum handed along 628 units)."""
+    """Config 5: final scene at 3840x2160 (16/9), 10000 spp — one row in one launch (60 tiles x 2439
+    sample chunks of rt_schedule.hpp, every pixel's running sum handed along 2438 units)."""
     cam = rtzig.final_scene_camera(width=3840, aspect_ratio=16 / 9, spp=10000)
     assert (cam.width, cam.height) == (3840, 2160)
     out, st, launches = _rows(cam, 1333, 1, 1)

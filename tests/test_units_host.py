@@ -1,4 +1,4 @@
-"""Host check of the unit scheduler's chunk schedule (csrc/rt_kernel.h "Work units"), CPU only."""
+"""Host check of the unit scheduler's chunk table (csrc/rt_schedule.hpp), CPU only."""
 import os
 import subprocess
 

@@ -65,6 +65,7 @@ for v in args.variants.split():
                         "first_drain_to_last_wave_end": round((s[15] - (~s[14] & (2**64 - 1))) / 100, 1)
                         if s[14] else None},
         "cycle_split": {"refill": round(s[4] / cyc, 4), "walk": round(s[5] / cyc, 4), "shade": round(s[6] / cyc, 4), "trips": round(s[16] / cyc, 4)},
+        "scheduler": {"idle_sleeps": s[17], "deferred_finalisations": s[18], "refills_without_free_slot": s[19]},
         "raw": s,
     }
     r.enable_profile(False)

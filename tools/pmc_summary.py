@@ -56,7 +56,9 @@ def main(tag, workload):
             disp.setdefault(c, set()).add(r["Dispatch_Id"])
             key = (c, r["Dispatch_Id"])
             dur[key] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9
-            out["vgpr"], out["sgpr"] = int(r["VGPR_Count"]), int(r["SGPR_Count"])
+            # rocprofv3's register fields as reported (VGPR_Count is not the compiler's count: the
+            # kernel compiles to 115 VGPRs, -Rpass-analysis=kernel-resource-usage, 4 waves / SIMD)
+            out["rocprof_VGPR_Count_field"], out["rocprof_SGPR_Count_field"] = int(r["VGPR_Count"]), int(r["SGPR_Count"])
     kt = lambda c: sum(v for (cc, _), v in dur.items() if cc == c)  # kernel seconds under counter c's pass
     g = lambda c: sums.get(c, float("nan"))
     out["launches_per_frame"] = len(disp.get("SQ_WAVES", disp.get("FETCH_SIZE", ())))
