@@ -30,7 +30,7 @@ constexpr uint32_t kMaxLdsSpheres = 2048;  // 64 KiB of LDS geometry; above this
 // Chunks: kUnitS samples each, shrinking towards the end of the launch (rt_schedule.hpp).
 // ------------------------------------------------------------------------------------------------
 constexpr uint32_t kUnitS = 16;  // samples per unit of the main chunks (ring slot size)
-constexpr uint32_t kSlots = 4;   // units a wave holds at once (3 measured equal; 2, 6, 8 slower)
+constexpr uint32_t kSlots = 4;   // units a wave holds at once (16 x 4 measured best)
 constexpr uint32_t kSlotMask = (1u << kSlots) - 1;
 constexpr uint32_t kRingSlotDoubles = kUnitS * 64 * 3;
 constexpr uint32_t kRingWaveDoubles = kSlots * kRingSlotDoubles;  // 96 KiB of f64 per wave

@@ -4,7 +4,7 @@ kernels by HIP events, inputs resident).  Config 5 (3840x2160, 10000 spp) runs a
 (--stress-spp) so the run stays short; the rate is per sample, and at 10000 spp only the number
 of units grows with spp (one launch per frame, in-kernel ordered accumulation).
 
-    python tools/configs_bench.py [--stress-spp 200] [--out profiles/r01_configs.json]
+    python tools/configs_bench.py [--stress-spp 200] [--out profiles/r02_configs.json]
 """
 import argparse
 import json
