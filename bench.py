@@ -214,7 +214,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed_max = float(t.item())
     kname = renderer.kernel_name()  # the timed (parity) kernel, before the fast-mode frames
-    k_sum, _, n_launch = renderer.kernel_times_total() if n_rows else (0.0, 0.0, 0)
+    k_sum, r_sum, n_launch = renderer.kernel_times_total() if n_rows else (0.0, 0.0, 0)
     st = stats.cpu().tolist()
     rays_per_frame = st[0] / max(1, args.steps)
     samples_per_frame = st[1] / max(1, args.steps)
@@ -264,7 +264,9 @@ def main():
         # write-through hand-off between sample chunks (24 B per pixel per chunk, both ways)
         alg_bytes = n_rows * W * (24 if args.output == "linear" else 3)
         frame_ms = elapsed_max / args.steps * 1e3
-        traffic = pmc.get("hbm_bytes_per_frame")
+        # the committed PMC passes profile the 1-GPU frame (ring mode); a rank's smaller row set runs
+        # in direct mode with different traffic, so N > 1 lines carry no PMC figure
+        traffic = pmc.get("hbm_bytes_per_frame") if world == 1 else None
         assert img is not None and img.shape[0] == H
         res = {
             "metric": METRIC,
@@ -308,6 +310,8 @@ def main():
                 "kernel_ms_per_frame": round(k_frame_s * 1e3, 3),
                 "launches_per_frame": round(launches_per_frame, 3),
                 "kernel_ms_avg": round(k_frame_s * 1e3 / max(1.0, launches_per_frame), 3),
+                "unit_mode": "direct" if "direct" in kname else "ring",
+                "reduce_ms_per_frame": round(r_sum / args.steps, 3),
             },
             "hbm": {
                 "algorithmic_bytes_per_frame": alg_bytes,
@@ -316,10 +320,13 @@ def main():
                 "frac": round(alg_bytes / (frame_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 7),
                 "pmc_bytes_per_frame": traffic,
                 "traffic_over_algorithmic": round(traffic / alg_bytes, 1) if traffic else None,
-                "overhead": "the in-kernel ordered accumulation: each sample's 24-B color written to and read "
-                            "back from its wave's ring (an upper bound of "
-                            f"{n_rows * W * spp * 48 / 1e9:.2f} GB per frame if none of it stays in L2 / MALL), "
-                            "and the running sums' write-through hand-off, 48 B per pixel per sample chunk",
+                "overhead": ("the in-kernel ordered accumulation: each sample's 24-B color written to and read "
+                             "back from its wave's ring (an upper bound of "
+                             f"{n_rows * W * spp * 48 / 1e9:.2f} GB per frame if none of it stays in L2 / MALL), "
+                             "and the running sums' write-through hand-off, 48 B per pixel per sample chunk")
+                            if "direct" not in kname else
+                            ("direct mode (small launch): every sample's 24-B color stored and read back once by "
+                             f"the reduce pass, {n_rows * W * spp * 48 / 1e9:.2f} GB per frame"),
             },
             "rays_per_sample": round(rays_per_frame / max(1, samples_per_frame), 4),
             "fixed_costs_ms": {"context_and_scene_upload": round(init_ms, 2)},

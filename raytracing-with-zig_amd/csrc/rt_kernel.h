@@ -28,24 +28,42 @@ constexpr uint32_t kMaxLdsSpheres = 2048;  // 64 KiB of LDS geometry; above this
 // sc1 stores, drained, then the flag: MI355X hand-off recipe, any XCD), or, for the last chunk,
 // writes the framebuffer (scale + optional Color.toRgb).  No per-sample buffer and no reduce pass.
 // Chunks: kUnitS samples each, shrinking towards the end of the launch (rt_schedule.hpp).
+//
+// DIRECT mode, for small launches (P x spp x 24 B within kDirectBytes: a rank's rows of a
+// multi-GPU job, the short book scenes): the items are numbered flat and sample-major,
+// t = s * P + q, and split into kSegs contiguous queue segments with a counter each; a wave claims a
+// run from its home segment with one atomic (guided: 1/8 of an even share of what the segment has
+// left, 64 to 2048 items), then from the other segments 64 at a time; a lane stores its color at
+// samples[t], and nothing waits on anything;
+// reduce_kernel then adds every pixel's stored colors in sample order.  Small launches have few
+// tiles: (tile, chunk) units would either be large (a long drain) or so many that the claim
+// counter's rate (≈88 claims per µs) bounds the launch.
 // ------------------------------------------------------------------------------------------------
 constexpr uint32_t kUnitS = 16;  // samples per unit of the main chunks (ring slot size)
 constexpr uint32_t kSlots = 4;   // units a wave holds at once (16 x 4 measured best)
 constexpr uint32_t kSlotMask = (1u << kSlots) - 1;
 constexpr uint32_t kRingSlotDoubles = kUnitS * 64 * 3;
 constexpr uint32_t kRingWaveDoubles = kSlots * kRingSlotDoubles;  // 96 KiB of f64 per wave
-constexpr size_t kCtrBytes = 256;  // [0] unit claim counter, [8] error word (zeroed per launch)
+// claim counters (zeroed per launch): ring mode ctr[0]; direct mode one per queue segment, each on
+// its own 128-B line, ctr[kCtrStride * seg]; then the error word ctr[kErrWord]
+constexpr uint32_t kSegs = 8;
+constexpr uint32_t kCtrStride = 16;
+constexpr uint32_t kErrWord = kSegs * kCtrStride;
+constexpr size_t kCtrBytes = (kErrWord + 16) * sizeof(unsigned long long);
+constexpr uint64_t kDirectBytes = 2ull << 30;  // direct mode when P x spp x 24 B fits
 
 struct UnitArgs {
     double* ring;              // [waves][kSlots][kUnitS * 64][3] wave-private sample colors
     double* sums;              // [P][3] running per-pixel sums (write-through hand-off between waves)
     uint32_t* flags;           // [n_tiles] chunks finalised per tile (zeroed per launch)
     void* out;                 // [P][3] f64 linear or u8 RGB (the last chunk's finalisation)
-    unsigned long long* ctr;   // kCtrBytes: [0] claim counter, [8] error word
+    unsigned long long* ctr;   // kCtrBytes: claim counters, [kErrWord] error word
     FastDiv div_tiles;         // u -> (chunk, tile)
     const uint32_t* chunk_s0;  // [n_chunks + 1]: chunk k covers samples [chunk_s0[k], chunk_s0[k + 1])
-    uint32_t n_tiles, n_units; // n_units = n_tiles * n_chunks < 2^32
-    uint32_t n_chunks, pad0;
+    double* samples;           // direct mode: [spp][P][3] every sample's color (reduce_kernel sums them)
+    FastDiv div_p;             // direct mode: / P, item t -> (sample, pixel)
+    uint32_t n_tiles, n_units; // n_units = n_tiles * n_chunks < 2^32 (direct mode: the P * spp items)
+    uint32_t n_chunks, spp;
     uint32_t P, out_format;    // pixels of the launch; 0 linear f64, 1 rgb8
     uint32_t ring_waves, pad;  // ring capacity in waves (the launch never has more)
     double scale;              // pixelSamplesScale
@@ -59,10 +77,7 @@ __device__ __forceinline__ void chunk_range(const UnitArgs& u, uint32_t k, uint3
 }
 
 constexpr uint32_t kPad = 4;               // sphere list padded to a multiple of this (sentinels)
-#ifndef RTZIG_RUV_TRIPS
-#define RTZIG_RUV_TRIPS 3
-#endif
-constexpr int kRuvTrips = RTZIG_RUV_TRIPS;  // randomUnitVec rejection trips per loop iteration (path_loop)
+constexpr int kRuvTrips = 3;  // randomUnitVec rejection trips per loop iteration (path_loop; 2, 4 slower)
 constexpr const char* kDefaultVariant = "smem_u4";  // see variant_choice() in rt_kernel.hip
 
 // Geometry walked by every lane for every ray: 32 B, one LDS broadcast pair per sphere.
@@ -159,6 +174,8 @@ __host__ __device__ inline uint32_t bvh_leaves_offset(uint32_t n_nodes) {
 
 // Launch wrappers (rt_kernel.hip, rt_kernel_fast.hip); asynchronous on `stream`.  The caller zeroes
 // ua->ctr (kCtrBytes) and ua->flags (n_tiles x 4 B) before every launch.
+// Direct mode's second pass: per pixel, the stored colors added in sample order, scaled, written.
+extern "C" hipError_t rtk_launch_reduce(const rtk::UnitArgs* ua, hipStream_t stream);
 extern "C" hipError_t rtk_launch_samples(const rtk::KernelParams* p, const rtk::GeoRec* geo,
                                          const rtk::MatRec* mat, const rtk::UnitArgs* ua,
                                          void* stats, hipStream_t stream, const char** name);

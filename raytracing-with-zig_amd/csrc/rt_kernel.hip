@@ -609,13 +609,13 @@ struct BvhWalker {
 // samples + the ordered finalisation of finished units.
 // `geo_orig` is the geometry in original list order (hit-record center of the winner).
 // ------------------------------------------------------------------------------------------------
-template <bool kProf, class Walker>
+template <bool kProf, bool kDirect, class Walker>
 __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& walk, const GeoRec* __restrict__ geo_orig,
                                           const MatRec* __restrict__ mat_g, const UnitArgs& ua,
                                           unsigned long long* __restrict__ stats) {
     const uint32_t W = p.width;
     const uint32_t lane = lane_id();
-    UnitSched us(ua, blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64);
+    UnitSched<kDirect> us(ua, blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64);
 
     // per-lane path state
     bool active = false;
@@ -896,7 +896,7 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
 }
 
 // Linear-walk kernel: geometry in LDS (kLds) or read by scalar loads from global memory.
-template <bool kLds, int U, int kWaves, bool kProf>
+template <bool kLds, int U, int kWaves, bool kProf, bool kDirect>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kWaves))) void sample_kernel(
     KernelParams p, const GeoRec* __restrict__ geo_g, const MatRec* __restrict__ mat_g, UnitArgs ua,
     unsigned long long* __restrict__ stats) {
@@ -907,12 +907,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kWaves))
         __syncthreads();
         geo = lds_geo;
     }
-    path_loop<kProf>(p, LinearWalker<U>{geo, p.n_pad, p.n_spheres}, geo, mat_g, ua, stats);
+    path_loop<kProf, kDirect>(p, LinearWalker<U>{geo, p.n_pad, p.n_spheres}, geo, mat_g, ua, stats);
 }
 
 // BVH-walk kernel: nodes + slot geometry + slot ids staged in LDS (kLdsScene) or read from global
 // memory; the per-lane traversal stack always lives in LDS.
-template <bool kLdsScene, bool kProf>
+template <bool kLdsScene, bool kProf, bool kDirect>
 __global__ __launch_bounds__(kBlockBvh) void sample_kernel_bvh(KernelParams p, BvhArgs b,
                                                                const GeoRec* __restrict__ geo_g,
                                                                const MatRec* __restrict__ mat_g, UnitArgs ua,
@@ -935,9 +935,41 @@ __global__ __launch_bounds__(kBlockBvh) void sample_kernel_bvh(KernelParams p, B
         nodes = ln;
         leaves = ll;
     }
-    path_loop<kProf>(p, BvhWalker<kLdsScene>{nodes, leaves, b.always_geo, b.always_sid, b.n_always, stack + threadIdx.x,
+    path_loop<kProf, kDirect>(p, BvhWalker<kLdsScene>{nodes, leaves, b.always_geo, b.always_sid, b.n_always, stack + threadIdx.x,
                                               b.origin_bound, geo_g, p.n_pad}, geo_g,
                      mat_g, ua, stats);
+}
+
+// Direct mode's second pass (rt_kernel.h "Work units"): thread q adds pixel q's stored colors in
+// sample order — pixelColor += rayColor(ray), camera.zig:133-136, from pixelColor = 0 — then
+// scales (:137) and writes linear f64 or the fused Color.toRgb bytes.  A wave's loads of one sample
+// are one contiguous 1536-B run; unrolled 8x to keep loads in flight (the order of the additions
+// is unchanged).
+template <int kOut>
+__global__ __launch_bounds__(256) void reduce_kernel(UnitArgs ua) {
+    const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= ua.P) return;
+    const double* src = ua.samples + 3 * (size_t)q;
+    const size_t stride = 3 * (size_t)ua.P;
+    double x = 0.0, y = 0.0, z = 0.0;
+#pragma unroll 8
+    for (uint32_t s = 0; s < ua.spp; ++s) {
+        x = x + src[0];
+        y = y + src[1];
+        z = z + src[2];
+        src += stride;
+    }
+    if constexpr (kOut == 0) {
+        double* o = (double*)ua.out + 3 * (size_t)q;
+        o[0] = x * ua.scale;
+        o[1] = y * ua.scale;
+        o[2] = z * ua.scale;
+    } else {
+        uint8_t* o = (uint8_t*)ua.out + 3 * (size_t)q;
+        o[0] = to_byte(x * ua.scale);
+        o[1] = to_byte(y * ua.scale);
+        o[2] = to_byte(z * ua.scale);
+    }
 }
 
 }  // namespace rtk
@@ -1001,7 +1033,9 @@ uint32_t grid_blocks(uint64_t need, uint64_t cap, const rtk::UnitArgs* ua, uint3
 template <bool kLds, int U, int kWaves>
 void launch_samples(const rtk::KernelParams* p, const rtk::GeoRec* geo, const rtk::MatRec* mat,
                     const rtk::UnitArgs* ua, unsigned long long* st, hipStream_t stream, size_t shmem, uint64_t need) {
-    auto kernel = p->prof ? rtk::sample_kernel<kLds, U, kWaves, true> : rtk::sample_kernel<kLds, U, kWaves, false>;
+    const bool direct = ua->samples != nullptr;
+    auto kernel = p->prof ? (direct ? rtk::sample_kernel<kLds, U, kWaves, true, true> : rtk::sample_kernel<kLds, U, kWaves, true, false>)
+                          : (direct ? rtk::sample_kernel<kLds, U, kWaves, false, true> : rtk::sample_kernel<kLds, U, kWaves, false, false>);
     const uint32_t blocks = grid_blocks(need, persistent_blocks(kernel, shmem), ua, rtk::kBlock);
     hipLaunchKernelGGL(kernel, dim3(blocks), dim3(rtk::kBlock), shmem, stream, *p, geo, mat, *ua, st);
 }
@@ -1073,8 +1107,27 @@ extern "C" hipError_t rtk_launch_samples_bvh(const rtk::KernelParams* p, const r
         hipLaunchKernelGGL(kernel, dim3(blocks), dim3(kBlockBvh), shmem, stream, *p, *b, geo, mat, *ua, st);
         return hipGetLastError();
     };
+    if (ua->samples != nullptr) {  // direct mode
+        if (p->prof)
+            return lds_scene ? launch(sample_kernel_bvh<true, true, true>, "bvh_lds(prof,direct)")
+                             : launch(sample_kernel_bvh<false, true, true>, "bvh_global(prof,direct)");
+        return lds_scene ? launch(sample_kernel_bvh<true, false, true>, "bvh_lds(direct)")
+                         : launch(sample_kernel_bvh<false, false, true>, "bvh_global(direct)");
+    }
     if (p->prof)
-        return lds_scene ? launch(sample_kernel_bvh<true, true>, "bvh_lds(prof)")
-                         : launch(sample_kernel_bvh<false, true>, "bvh_global(prof)");
-    return lds_scene ? launch(sample_kernel_bvh<true, false>, "bvh_lds") : launch(sample_kernel_bvh<false, false>, "bvh_global");
+        return lds_scene ? launch(sample_kernel_bvh<true, true, false>, "bvh_lds(prof)")
+                         : launch(sample_kernel_bvh<false, true, false>, "bvh_global(prof)");
+    return lds_scene ? launch(sample_kernel_bvh<true, false, false>, "bvh_lds")
+                     : launch(sample_kernel_bvh<false, false, false>, "bvh_global");
+}
+
+extern "C" hipError_t rtk_launch_reduce(const rtk::UnitArgs* ua, hipStream_t stream) {
+    using namespace rtk;
+    if (ua->P == 0 || ua->samples == nullptr) return hipErrorInvalidValue;
+    const uint32_t blocks = (ua->P + 255) / 256;
+    if (ua->out_format == 0)
+        hipLaunchKernelGGL(reduce_kernel<0>, dim3(blocks), dim3(256), 0, stream, *ua);
+    else
+        hipLaunchKernelGGL(reduce_kernel<1>, dim3(blocks), dim3(256), 0, stream, *ua);
+    return hipGetLastError();
 }

@@ -308,7 +308,7 @@ struct Walker {
     }
 };
 
-template <class Walker>
+template <bool kDirect, class Walker>
 __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& walk, const GeoRec* __restrict__ geo_orig,
                                           const MatRec* __restrict__ mat_g, const UnitArgs& ua,
                                           unsigned long long* __restrict__ stats) {
@@ -316,7 +316,7 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
     const uint32_t lane = lane_id();
     const float t_min = (float)p.t_min, t_max = (float)p.t_max;
 
-    UnitSched us(ua, blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64);  // as the parity kernel
+    UnitSched<kDirect> us(ua, blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64);  // as the parity kernel
     bool active = false, pending = false, sc_metal = false, dpend = false;
     uint32_t myslot = 0, mi = 0;
     Rng g;
@@ -468,7 +468,7 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
     }
 }
 
-template <bool kLdsScene>
+template <bool kLdsScene, bool kDirect>
 __global__ __launch_bounds__(kBlockBvh) void sample_kernel_fast(KernelParams p, BvhArgs b,
                                                                 const GeoRec* __restrict__ geo_g,
                                                                 const MatRec* __restrict__ mat_g, UnitArgs ua,
@@ -489,7 +489,7 @@ __global__ __launch_bounds__(kBlockBvh) void sample_kernel_fast(KernelParams p, 
         nodes = ln;
         leaves = ll;
     }
-    path_loop(p, Walker<kLdsScene>{nodes, leaves, b.always_geo, b.always_sid, b.n_always, stack + threadIdx.x, b.origin_bound},
+    path_loop<kDirect>(p, Walker<kLdsScene>{nodes, leaves, b.always_geo, b.always_sid, b.n_always, stack + threadIdx.x, b.origin_bound},
               geo_g, mat_g, ua, stats);
 }
 
@@ -519,5 +519,9 @@ extern "C" hipError_t rtk_launch_samples_fast(const rtk::KernelParams* p, const 
                            (unsigned long long*)stats);
         return hipGetLastError();
     };
-    return lds_scene ? launch(rtf::sample_kernel_fast<true>, "fast_f32_lds") : launch(rtf::sample_kernel_fast<false>, "fast_f32_global");
+    if (ua->samples != nullptr)  // direct mode
+        return lds_scene ? launch(rtf::sample_kernel_fast<true, true>, "fast_f32_lds(direct)")
+                         : launch(rtf::sample_kernel_fast<false, true>, "fast_f32_global(direct)");
+    return lds_scene ? launch(rtf::sample_kernel_fast<true, false>, "fast_f32_lds")
+                     : launch(rtf::sample_kernel_fast<false, false>, "fast_f32_global");
 }

@@ -72,11 +72,13 @@ struct rt_context {
     size_t sums_bytes = 0;
     uint32_t* d_flags = nullptr;
     size_t flags_bytes = 0;
+    double* d_samples = nullptr;    // direct mode: [spp][P][3] (at most rtk::kDirectBytes)
+    size_t samples_bytes = 0;
     std::vector<uint32_t> sched;    // chunk table of the last launch (rt_schedule.hpp), and its copy
     uint32_t* d_sched = nullptr;
     size_t sched_bytes = 0;
     uint64_t sched_lanes = 0;       // resident lanes the schedule is sized for (CUs x 16 waves x 64)
-    unsigned long long* d_ctr = nullptr;  // rtk::kCtrBytes, zeroed per launch ([8]: error word)
+    unsigned long long* d_ctr = nullptr;  // rtk::kCtrBytes, zeroed per launch ([kErrWord]: error word)
     const char* last_kernel = "sample_kernel";
     SceneData scene;                // host copy (BVH rebuilds for far-away cameras, scene comparisons)
     rtk::BvhArgs bvh{};
@@ -94,7 +96,7 @@ struct rt_context {
     bool timing = false;
     bool profile = false;  // instrumented kernels: d_stats must hold 24 uint64 (rt.h)
     int precision = RT_PRECISION_F64;
-    std::vector<hipEvent_t> events;  // 2 per timed launch: start, stop
+    std::vector<hipEvent_t> events;  // 3 per timed call: start, sample kernel done, reduce done
     uint32_t call_first = 0;
     uint32_t timed_calls = 0;
     uint32_t log_used = 0;
@@ -446,7 +448,7 @@ int rt_context_destroy(rt_context* ctx) {
     if (ctx->done_valid) (void)hipEventSynchronize(ctx->done);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     for (void* p : {(void*)ctx->d_geo, (void*)ctx->d_mat, (void*)ctx->d_ring, (void*)ctx->d_sums, (void*)ctx->d_flags,
-                    (void*)ctx->d_sched, (void*)ctx->d_ctr, (void*)ctx->d_nodes, (void*)ctx->d_leaves, (void*)ctx->d_always_geo,
+                    (void*)ctx->d_samples, (void*)ctx->d_sched, (void*)ctx->d_ctr, (void*)ctx->d_nodes, (void*)ctx->d_leaves, (void*)ctx->d_always_geo,
                     (void*)ctx->d_always_sid, ctx->d_out, (void*)ctx->d_stats})
         (void)hipFree(p);
     if (ctx->h_out) (void)hipHostFree(ctx->h_out);
@@ -473,7 +475,7 @@ int rt_context_sync(rt_context* ctx) {
     int rc = quiesce(ctx);
     if (rc || !ctx->d_ctr) return rc;
     unsigned long long err = 0;
-    HIP_CHECK(hipMemcpy(&err, ctx->d_ctr + 8, sizeof err, hipMemcpyDeviceToHost));
+    HIP_CHECK(hipMemcpy(&err, ctx->d_ctr + rtk::kErrWord, sizeof err, hipMemcpyDeviceToHost));
     if (err) {
         rt_set_last_error("render kernel: a wave timed out waiting for a running-sum hand-off");
         return RT_ERR_HIP;
@@ -525,9 +527,27 @@ int rt_render_rows_async(rt_context* ctx, const rt_camera* cam, uint32_t output_
         rt_set_last_error("too many work units (rows x samples): render fewer rows per call");
         return RT_ERR_CAPACITY;
     }
-    rc = ensure_buffer(ctx, (void**)&ctx->d_ring, &ctx->ring_bytes,
-                       (size_t)ctx->ring_waves * rtk::kRingWaveDoubles * sizeof(double));
-    if (!rc && ua.n_chunks > 1) rc = ensure_buffer(ctx, (void**)&ctx->d_sums, &ctx->sums_bytes, P * 3 * sizeof(double));
+    // direct mode for small launches (rt_kernel.h "Work units"); RTZIG_UNIT_MODE=ring|direct forces
+    // one (test hook: both paths on the same inputs)
+    const uint64_t direct_bytes = P * (uint64_t)cam->samples_per_pixel * 3 * sizeof(double);
+    bool direct = direct_bytes <= rtk::kDirectBytes;
+    if (const char* e = std::getenv("RTZIG_UNIT_MODE")) {
+        if (std::strcmp(e, "ring") == 0) direct = false;
+        if (std::strcmp(e, "direct") == 0) {
+            if (direct_bytes > (16ull << 30)) {
+                rt_set_last_error("RTZIG_UNIT_MODE=direct: launch needs more than 16 GiB of sample storage");
+                return RT_ERR_CAPACITY;
+            }
+            direct = true;
+        }
+    }
+    if (direct) {
+        rc = ensure_buffer(ctx, (void**)&ctx->d_samples, &ctx->samples_bytes, direct_bytes);
+    } else {
+        rc = ensure_buffer(ctx, (void**)&ctx->d_ring, &ctx->ring_bytes,
+                           (size_t)ctx->ring_waves * rtk::kRingWaveDoubles * sizeof(double));
+        if (!rc && ua.n_chunks > 1) rc = ensure_buffer(ctx, (void**)&ctx->d_sums, &ctx->sums_bytes, P * 3 * sizeof(double));
+    }
     const size_t flag_bytes = (n_tiles * sizeof(uint32_t) + 15) & ~(size_t)15;  // memset in 16-B multiples
     if (!rc) rc = ensure_buffer(ctx, (void**)&ctx->d_flags, &ctx->flags_bytes, flag_bytes);
     if (!rc && !ctx->d_ctr) {
@@ -535,13 +555,16 @@ int rt_render_rows_async(rt_context* ctx, const rt_camera* cam, uint32_t output_
         rc = ensure_buffer(ctx, (void**)&ctx->d_ctr, &cb, rtk::kCtrBytes);
     }
     if (rc) return rc;
-    ua.ring = ctx->d_ring;
-    ua.sums = ctx->d_sums;
+    ua.ring = direct ? nullptr : ctx->d_ring;
+    ua.sums = direct ? nullptr : ctx->d_sums;
+    ua.samples = direct ? ctx->d_samples : nullptr;
+    ua.spp = cam->samples_per_pixel;
     ua.flags = ctx->d_flags;
     ua.out = d_out;
     ua.ctr = ctx->d_ctr;
     ua.n_tiles = (uint32_t)n_tiles;
-    ua.n_units = (uint32_t)(n_tiles * ua.n_chunks);
+    ua.n_units = direct ? (uint32_t)(P * cam->samples_per_pixel) : (uint32_t)(n_tiles * ua.n_chunks);
+    ua.div_p = rtk::fastdiv_make((uint32_t)P);
     ua.div_tiles = rtk::fastdiv_make((uint32_t)n_tiles);
     ua.P = (uint32_t)P;
     ua.out_format = output_format;
@@ -552,7 +575,7 @@ int rt_render_rows_async(rt_context* ctx, const rt_camera* cam, uint32_t output_
         if (ctx->log_used + 1 > kMaxTimed) ctx->log_used = 0;  // wrap: totals restart
         ctx->call_first = ctx->log_used;
         ctx->log_used += 1;
-        while (ctx->events.size() < 2 * (size_t)ctx->log_used) {
+        while (ctx->events.size() < 3 * (size_t)ctx->log_used) {
             hipEvent_t e;
             HIP_CHECK(make_event(&e, true));
             ctx->events.push_back(e);
@@ -562,13 +585,13 @@ int rt_render_rows_async(rt_context* ctx, const rt_camera* cam, uint32_t output_
     // a previous render of this context on another stream may still use the buffers
     if (ctx->done_valid && ctx->done_stream != s) HIP_CHECK(hipStreamWaitEvent(s, ctx->done, 0));
     HIP_CHECK(hipMemsetAsync(ctx->d_ctr, 0, rtk::kCtrBytes, s));
-    HIP_CHECK(hipMemsetAsync(ctx->d_flags, 0, flag_bytes, s));
+    if (!direct) HIP_CHECK(hipMemsetAsync(ctx->d_flags, 0, flag_bytes, s));
     const bool bvh = use_bvh(ctx);
     rtk::KernelParams p = make_params(cam, row0, row_step, n_rows, ctx->n_spheres);
     p.prof = ctx->profile && d_stats ? 1u : 0u;
     p.s_begin = 0;
     p.s_count = cam->samples_per_pixel;
-    hipEvent_t* ev = ctx->timing ? &ctx->events[2 * ctx->call_first] : nullptr;
+    hipEvent_t* ev = ctx->timing ? &ctx->events[3 * ctx->call_first] : nullptr;
     if (ev) HIP_CHECK(hipEventRecord(ev[0], s));
     if (bvh && ctx->precision == RT_PRECISION_F32)
         HIP_CHECK(rtk_launch_samples_fast(&p, &ctx->bvh, ctx->d_geo, ctx->d_mat, &ua, d_stats, s, &ctx->last_kernel));
@@ -577,6 +600,8 @@ int rt_render_rows_async(rt_context* ctx, const rt_camera* cam, uint32_t output_
     else
         HIP_CHECK(rtk_launch_samples(&p, ctx->d_geo, ctx->d_mat, &ua, d_stats, s, &ctx->last_kernel));
     if (ev) HIP_CHECK(hipEventRecord(ev[1], s));
+    if (direct) HIP_CHECK(rtk_launch_reduce(&ua, s));
+    if (ev) HIP_CHECK(hipEventRecord(ev[2], s));
     HIP_CHECK(hipEventRecord(ctx->done, s));
     ctx->done_valid = true;
     ctx->done_stream = s;
@@ -610,15 +635,17 @@ int rt_context_enable_profile(rt_context* ctx, int enable) {
 
 static int sum_times(rt_context* ctx, uint32_t first, uint32_t count, double* sample_ms, double* reduce_ms) {
     HIP_CHECK(hipSetDevice(ctx->device));
-    double sm = 0;
+    double sm = 0, rm = 0;
     for (uint32_t c = first; c < first + count; c++) {
-        float a = 0;
-        HIP_CHECK(hipEventSynchronize(ctx->events[2 * c + 1]));
-        HIP_CHECK(hipEventElapsedTime(&a, ctx->events[2 * c + 0], ctx->events[2 * c + 1]));
+        float a = 0, b = 0;
+        HIP_CHECK(hipEventSynchronize(ctx->events[3 * c + 2]));
+        HIP_CHECK(hipEventElapsedTime(&a, ctx->events[3 * c + 0], ctx->events[3 * c + 1]));
+        HIP_CHECK(hipEventElapsedTime(&b, ctx->events[3 * c + 1], ctx->events[3 * c + 2]));
         sm += a;
+        rm += b;
     }
     if (sample_ms) *sample_ms = sm;
-    if (reduce_ms) *reduce_ms = 0.0;  // no reduce pass: the sample kernel accumulates in order itself
+    if (reduce_ms) *reduce_ms = rm;  // direct mode's reduce pass (ring mode: an empty interval)
     return RT_OK;
 }
 
@@ -753,7 +780,7 @@ int rt_render(const rt_camera* cam, const rt_sphere* spheres, size_t n, const rt
         if (rc) return rc;
         HIP_CHECK(hipMemcpyAsync(c->h_out, c->d_out, bytes, hipMemcpyDeviceToHost, c->stream));
         HIP_CHECK(hipMemcpyAsync(c->h_stats, c->d_stats, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
-        HIP_CHECK(hipMemcpyAsync(c->h_stats + 2, c->d_ctr + 8, sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
+        HIP_CHECK(hipMemcpyAsync(c->h_stats + 2, c->d_ctr + rtk::kErrWord, sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
     }
     uint64_t stats[2] = {0, 0};
     for (int g = 0; g < G; g++) {

@@ -31,11 +31,14 @@ __device__ __forceinline__ void st_wt(double* p, double v) {  // global_store_dw
 
 // A wave that cannot claim and has nothing to trace sleeps between polls; a bug that broke the
 // dependency chain would otherwise hang the GPU, so the wait is bounded (≈ 0.5 s of sleeping per
-// wave): past it the wave reports it in ctr[8] and gives up (the host returns RT_ERR_HIP).
+// wave): past it the wave reports it in ctr[kErrWord] and gives up (the host returns RT_ERR_HIP).
 constexpr uint32_t kSpinLimit = 1u << 22;
 
 
-// Wave-uniform scheduler state (every member is the same in all 64 lanes).
+// Wave-uniform scheduler state (every member is the same in all 64 lanes).  kDirect: direct mode
+// (rt_kernel.h): guided claims of flat items t = s * P + q (also the item's index in ua.samples);
+// no slots, no finalisation.
+template <bool kDirect>
 struct UnitSched {
     const UnitArgs& ua;
     double* ring;                    // this wave's ring: kSlots x [kUnitS * 64][3]
@@ -44,20 +47,58 @@ struct UnitSched {
     uint32_t cur_tile = 0, cur_s0 = 0;
     uint32_t st_u[kSlots];           // unit id held by each slot
     uint32_t spins = 0;
+    uint32_t seen = 0;               // direct mode: item position after this wave's last claim
+    uint32_t waves = 1;              // direct mode: the launch's waves
+    uint32_t seg = 0, empty = 0;     // direct mode: segment claimed from; segments found empty
+    bool away = false;               // direct mode: claiming outside the home segment
     uint32_t n_dep_wait = 0;   // diagnostics (instrumented build): finalisations deferred on a flag
     uint32_t n_no_slot = 0;    // ... refills stopped for want of a free slot
     bool drained = false;            // the claim counter is exhausted
-    bool failed = false;             // spin limit reached (reported in ctr[8])
+    bool failed = false;             // spin limit reached (reported in ctr[kErrWord])
 
     __device__ UnitSched(const UnitArgs& a, uint32_t wave) : ua(a), ring(a.ring + (size_t)wave * kRingWaveDoubles) {
+        if constexpr (kDirect) {
+            waves = gridDim.x * (blockDim.x / 64);
+            seg = blockIdx.x % kSegs;
+            seen = seg_lo(seg);
+        }
 #pragma unroll
         for (uint32_t j = 0; j < kSlots; ++j) st_u[j] = 0;
     }
-    __device__ __forceinline__ bool can_claim() const { return !drained && (~busy & kSlotMask) != 0; }
+    // direct mode: first item of queue segment g (segments split the P * spp items evenly)
+    __device__ __forceinline__ uint32_t seg_lo(uint32_t g) const {
+        return (uint32_t)((uint64_t)ua.n_units * g / kSegs);
+    }
+    __device__ __forceinline__ bool can_claim() const { return !drained && (kDirect || (~busy & kSlotMask) != 0); }
 
     // Claims the next unit into a free slot and makes it the one handed out; false if there is no
     // free slot or no unit left.
     __device__ __forceinline__ bool claim(uint32_t lane) {
+        if constexpr (kDirect) {
+            while (!drained) {
+                const uint32_t lo = seg_lo(seg), hi = seg_lo(seg + 1);
+                // guided in the home segment: 1/8 of an even share of what it has left (as this
+                // wave last saw it; its kSegs-th of the waves claim there), 64..2048 items in whole
+                // multiples of 64; elsewhere 64
+                const uint32_t left = hi > seen ? hi - seen : 0u;
+                uint32_t k = away ? 64u : left / waves;
+                k = k < 64u ? 64u : (k > 2048u ? 2048u : k & ~63u);
+                uint32_t t = 0;
+                if (lane == 0) t = (uint32_t)atomicAdd(ua.ctr + kCtrStride * seg, (unsigned long long)k);
+                t = lo + __builtin_amdgcn_readfirstlane(t);
+                if (t < hi) {
+                    seen = t + k;
+                    cur = t;
+                    end = hi - t < k ? hi : t + k;
+                    empty = 0;
+                    return true;
+                }
+                if (++empty >= kSegs) drained = true;
+                seg = seg + 1 == kSegs ? 0u : seg + 1;
+                away = true;
+            }
+            return false;
+        }
         const uint32_t freem = ~busy & kSlotMask;
         if (drained) return false;
         if (freem == 0) {
@@ -102,14 +143,23 @@ struct UnitSched {
                                                               __builtin_amdgcn_mbcnt_lo((uint32_t)needy, 0u));
                 if (rk < take) {
                     const uint32_t m = cur + rk;
-                    const uint32_t pq = cur_tile * 64 + (m & 63);
-                    if (pq < ua.P) {
-                        myslot = cur_slot;
+                    if constexpr (kDirect) {
+                        s = fastdiv(m, ua.div_p);
+                        q = m - s * ua.P;
                         mi = m;
-                        q = pq;
-                        s = cur_s0 + (m >> 6);
+                        myslot = 0;
                         active = true;
                         fresh = true;
+                    } else {
+                        const uint32_t pq = cur_tile * 64 + (m & 63);
+                        if (pq < ua.P) {
+                            myslot = cur_slot;
+                            q = pq;
+                            s = cur_s0 + (m >> 6);
+                            mi = m;
+                            active = true;
+                            fresh = true;
+                        }
                     }
                 }
             }
@@ -118,9 +168,10 @@ struct UnitSched {
         }
     }
 
-    // The color of a finished item goes to its unit's ring slot: [slot][m][3].
+    // The color of a finished item goes to its unit's ring slot: [slot][m][3] (direct mode:
+    // samples[m = s * P + q]).
     __device__ __forceinline__ void store(uint32_t slot, uint32_t m, double x, double y, double z) const {
-        double* d = ring + (size_t)slot * kRingSlotDoubles + 3 * m;
+        double* d = kDirect ? ua.samples + 3 * (size_t)m : ring + (size_t)slot * kRingSlotDoubles + 3 * m;
         d[0] = x;
         d[1] = y;
         d[2] = z;
@@ -128,6 +179,7 @@ struct UnitSched {
 
     // Slots whose unit has been handed out completely and has no item in flight in any lane.
     __device__ __forceinline__ uint32_t ready_mask(bool active, uint32_t myslot) const {
+        if constexpr (kDirect) return 0;
         uint32_t ready = 0;
 #pragma unroll
         for (uint32_t j = 0; j < kSlots; ++j) {
@@ -138,7 +190,7 @@ struct UnitSched {
     }
 
     __device__ __forceinline__ bool finalize_one(uint32_t ready, uint32_t lane) {
-        if (ready == 0) return false;
+        if (kDirect || ready == 0) return false;
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's ring stores have completed
         while (ready) {
             const uint32_t j = (uint32_t)__builtin_ctz(ready);
@@ -204,7 +256,7 @@ struct UnitSched {
     // Nothing to trace in this wave: wait for a dependency (bounded).  False: give up (reported).
     __device__ __forceinline__ bool wait(uint32_t lane) {
         if (++spins > kSpinLimit) {
-            if (lane == 0) atomicOr(ua.ctr + 8, 1ull);
+            if (lane == 0) atomicOr(ua.ctr + kErrWord, 1ull);
             failed = true;
             return false;
         }

@@ -1,6 +1,7 @@
 """Every BASELINE.json GPU config at its STATED spp (SURVEY §8(d) parity targets), through the C ABI.
 
-* bit-exact against oracle B (the reference arithmetic with the GPU's per-(pixel, sample) streams):
+* bit-exact against oracle B (the reference arithmetic with the GPU's per-(pixel, sample) streams),
+  in both unit modes (ring: in-kernel ordered accumulation; direct: stored samples + reduce pass):
   config 2 whole image at 100 spp; configs 3 and 4 on 8 interleaved rows at 500 spp; config 5 on one
   row at 10000 spp (2439 sample chunks: the in-kernel ordered accumulation hands each pixel's running
   sum from unit to unit, camera.zig:133-136);
@@ -38,8 +39,11 @@ def _rows(cam, row0, step, n):
     return buf.cpu().numpy(), [int(x) for x in stats.cpu().tolist()], launches
 
 
-def test_config2_full_image_100spp_bit_exact(oracle):
-    """Config 2: chapter 9 (two Lambertian spheres), 400x225, 100 spp, depth 50 — every pixel."""
+@pytest.mark.parametrize("mode", ["ring", "direct"])
+def test_config2_full_image_100spp_bit_exact(oracle, mode, monkeypatch):
+    """Config 2: chapter 9 (two Lambertian spheres), 400x225, 100 spp, depth 50 — every pixel, in
+    both unit modes (direct is the default at this size)."""
+    monkeypatch.setenv("RTZIG_UNIT_MODE", mode)
     cam = rtzig.chapter9_camera(spp=100)
     st = {}
     out = rtzig.render(cam.cam, cam.scene.world, n_gpus=1, stats=st)
@@ -62,8 +66,10 @@ def test_configs2_3_statistically_match_reference_images(oracle, golden_dir, con
     assert _box_rmse(gpu, gold) <= 1.5 * floor, (_box_rmse(gpu, gold), floor)
 
 
-def test_config3_rows_500spp_bit_exact(oracle):
+@pytest.mark.parametrize("mode", ["ring", "direct"])
+def test_config3_rows_500spp_bit_exact(oracle, mode, monkeypatch):
     """Config 3: chapter 13 scene + camera, 1200x675, 500 spp — 8 rows spread over the image."""
+    monkeypatch.setenv("RTZIG_UNIT_MODE", mode)
     cam = rtzig.chapter13_camera(width=1200, spp=500)
     assert (cam.width, cam.height) == (1200, 675)
     out, st, _ = _rows(cam, 3, 83, 8)
@@ -72,8 +78,10 @@ def test_config3_rows_500spp_bit_exact(oracle):
     assert st == [rays, 8 * 1200 * 500]
 
 
-def test_config4_rows_500spp_bit_exact(oracle):
+@pytest.mark.parametrize("mode", ["ring", "direct"])
+def test_config4_rows_500spp_bit_exact(oracle, mode, monkeypatch):
     """Config 4 (the bench workload): final scene, 1200x800, 500 spp — 8 rows spread over the image."""
+    monkeypatch.setenv("RTZIG_UNIT_MODE", mode)
     cam = rtzig.final_scene_camera(width=1200, aspect_ratio=1.5, spp=500)
     assert (cam.width, cam.height, len(cam.scene.world)) == (1200, 800, 485)
     out, st, _ = _rows(cam, 7, 99, 8)
@@ -82,13 +90,16 @@ def test_config4_rows_500spp_bit_exact(oracle):
     assert st == [rays, 8 * 1200 * 500]
 
 
-def test_config5_row_10000spp_bit_exact(oracle):
+@pytest.mark.parametrize("mode", ["ring", "direct"])
+def test_config5_row_10000spp_bit_exact(oracle, mode, monkeypatch):
     """Config 5: final scene at 3840x2160 (16/9), 10000 spp — one row in one launch (60 tiles x 2439
-    sample chunks of rt_schedule.hpp, every pixel's running sum handed along 2438 units)."""
+    sample chunks of rt_schedule.hpp, every pixel's running sum handed along 2438 units in ring
+    mode; direct mode stores the row's 3.84e7 samples, 0.92 GB, and reduces them)."""
+    monkeypatch.setenv("RTZIG_UNIT_MODE", mode)
     cam = rtzig.final_scene_camera(width=3840, aspect_ratio=16 / 9, spp=10000)
     assert (cam.width, cam.height) == (3840, 2160)
     out, st, launches = _rows(cam, 1333, 1, 1)
-    assert launches == 1
+    assert launches == 1  # one sample-kernel launch (+ the reduce pass in direct mode)
     ref, rays = oracle.render_b(cam.cam, cam.scene.world, row0=1333, row_step=1, n_rows=1, threads=16)
     assert np.array_equal(out, ref)
     assert st == [rays, 3840 * 10000]

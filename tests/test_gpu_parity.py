@@ -218,11 +218,13 @@ def test_c_harness_end_to_end(tmp_path):
     assert open(out, "rb").read() == rtzig.encode_p6(rgb, 400, 225)
 
 
+@pytest.mark.parametrize("mode", ["ring", "direct"])
 @pytest.mark.parametrize("variant", ["bvh", "smem_u4", "lds_u4"])
-def test_walk_variants_bit_exact(oracle, variant, monkeypatch):
-    """Every closest-hit walk (BVH and the linear list walks) gives oracle B's bits: golden config
-    + the degenerate-materials scene."""
+def test_walk_variants_bit_exact(oracle, variant, mode, monkeypatch):
+    """Every closest-hit walk (BVH and the linear list walks) gives oracle B's bits in both unit
+    modes (separate kernel instantiations): golden config + the degenerate-materials scene."""
     monkeypatch.setenv("RTZIG_KERNEL", variant)
+    monkeypatch.setenv("RTZIG_UNIT_MODE", mode)
     cam = rtzig.final_scene_camera(width=200, aspect_ratio=16 / 9, spp=6)
     out, st = gpu_render(cam, cam.scene.world, n_gpus=1)
     ref, rays = oracle.render_b(cam.cam, cam.scene.world, threads=8)
@@ -355,11 +357,14 @@ def test_kernel_times_total_accumulates():
     r.close()
 
 
+@pytest.mark.parametrize("mode", ["ring", "direct"])
 @pytest.mark.parametrize("spp", [1, 2, 3, 15, 16, 17, 31, 33, 47, 100])
-def test_unit_schedule_sample_counts_bit_exact(oracle, spp):
-    """Every chunk schedule shape of the unit scheduler (rt_kernel.h "Work units": main chunks of 16
-    samples, then a halving tail) on an image whose pixel count is not a multiple of 64 (a partial
-    last tile): the in-kernel ordered accumulation must give oracle B's bits."""
+def test_unit_schedule_sample_counts_bit_exact(oracle, spp, mode, monkeypatch):
+    """Every chunk schedule shape of the unit scheduler (rt_kernel.h "Work units": chunks of up to 16
+    samples, shrinking towards the end, rt_schedule.hpp) on an image whose pixel count is not a
+    multiple of 64 (a partial last tile), in both modes: the ring's in-kernel ordered accumulation
+    and direct mode's stored samples + reduce pass must give oracle B's bits."""
+    monkeypatch.setenv("RTZIG_UNIT_MODE", mode)
     cam = rtzig.final_scene_camera(width=37, aspect_ratio=16 / 9, spp=spp)
     out, st = gpu_render(cam, cam.scene.world, n_gpus=1)
     ref, rays = oracle.render_b(cam.cam, cam.scene.world, threads=16)
@@ -370,10 +375,12 @@ def test_unit_schedule_sample_counts_bit_exact(oracle, spp):
 
 
 @pytest.mark.parametrize("width,spp", [(8, 300), (64, 120), (1, 700)])
-def test_running_sum_handoff_chains(oracle, width, spp):
+def test_running_sum_handoff_chains(oracle, width, spp, monkeypatch):
     """One or a few tiles with many sample chunks: consecutive units of the SAME tile are claimed
     back to back by different waves, so nearly every finalisation waits on the previous chunk's
-    hand-off (write-through sums + per-tile flag, rt_units.h)."""
+    hand-off (write-through sums + per-tile flag, rt_units.h).  Ring mode forced (such small
+    launches run in direct mode by default)."""
+    monkeypatch.setenv("RTZIG_UNIT_MODE", "ring")
     cam = (rtzig.Camera.builder(width, 1.0).setScene(rtzig.Scene.init(0x5eed).generateWorld())
            .setDefocusAngle(0.6).setFocusDist(10).setViewport((13, 2, 3), (0, 0, 0), 20)
            .setSamplesPerPixel(spp).build())

@@ -22,9 +22,15 @@ ap.add_argument("--spp", type=int, default=100)
 ap.add_argument("--variants", default="bvh smem_u4")
 ap.add_argument("--rows", default=None, help="row0:step:n (rank rehearsal), default: the whole image")
 ap.add_argument("--out", default=None)
+ap.add_argument("--scene", choices=["final", "ch9", "ch13"], default="final")
 args = ap.parse_args()
 
-cam = rtzig.final_scene_camera(width=args.width, aspect_ratio=args.aspect, spp=args.spp)
+if args.scene == "ch9":
+    cam = rtzig.chapter9_camera(width=args.width, spp=args.spp)
+elif args.scene == "ch13":
+    cam = rtzig.chapter13_camera(width=args.width, spp=args.spp)
+else:
+    cam = rtzig.final_scene_camera(width=args.width, aspect_ratio=args.aspect, spp=args.spp)
 H, W = cam.height, cam.width
 r = rtzig.DeviceRenderer(0)
 r.set_scene(cam.scene.world)
@@ -37,6 +43,7 @@ res = {"config": f"{W}x{H} {args.spp}spp, {len(cam.scene.world)} spheres", "vari
 for v in args.variants.split():
     os.environ["RTZIG_KERNEL"] = v
     r.enable_profile(False)
+    r.render_rows_async(cam.cam, out.data_ptr(), **rows)  # warm-up (code object, BVH, workspace)
     r.render_rows_async(cam.cam, out.data_ptr(), **rows)
     torch.cuda.synchronize()
     plain_ms, _ = r.kernel_times()

@@ -3,7 +3,8 @@
 N = 1, 2, 4, 8, so the efficiency the 8-GPU driver will measure can be predicted without 8 GPUs.
 
 Per N:
-  * kernel: the sample kernel's HIP-event time for EVERY rank's interleaved row set (rows r, r+N, ...)
+  * kernel: the HIP-event time of the sample kernel (+ direct mode's reduce pass) for EVERY rank's
+    interleaved row set (rows r, r+N, ...)
     — the bench takes the max over ranks, so the prediction does too;
   * gather: rank 0's share of `rdist.gather_image` — the assemble copy (measured here on rank 0's
     buffer of N x R x W x 3 f64) plus the transfer of the N-1 peers' rows over xGMI (modelled: each
@@ -47,7 +48,7 @@ def kernel_ms(row0, step, n_rows):
     ks = []
     for _ in range(args.reps):
         r.render_rows_async(cam.cam, out.data_ptr(), row0=row0, row_step=step, n_rows=n_rows)
-        ks.append(r.kernel_times()[0])
+        ks.append(sum(r.kernel_times()))  # sample kernel + direct mode's reduce pass
     return min(ks)
 
 
