@@ -133,23 +133,7 @@ struct KernelParams {
 // on 32 different banks of the 64 (gcd(26, 64) = 2), so per-lane random ds_read_b64 gathers
 // spread over the whole bank row.  Leaves (2 slots: 80 B = 5 x 16, read as ds_read_b128) start
 // at the next 16-B boundary after the nodes.
-#ifndef RTZIG_BVH4
-#define RTZIG_BVH4 0
-#endif
-#if RTZIG_BVH4
-// EXPERIMENT: 4-wide nodes (two BvhNode slots each), one 1024-thread block per CU (deeper stacks)
-struct alignas(8) BvhNode4 {
-    float c[4][3][4];  // child c, axis: {lo, hi, hi, lo}
-    int32_t ref[4];
-};  // 208 B
-constexpr int kBlockBvh = 1024;
-constexpr size_t kLdsBudgetBvh = 160 * 1024;
-constexpr int kMaxStackBvh = 32;
-#else
 constexpr int kBlockBvh = 512;     // 8 waves; 2 blocks per CU share the LDS budget
-constexpr size_t kLdsBudgetBvh = 80 * 1024;
-constexpr int kMaxStackBvh = 16;
-#endif
 constexpr int kMaxDepthBvh = 16;   // == rtbvh::kMaxDepth: bound on per-lane LDS stack entries (entry 0: "done")
 #ifndef RTZIG_LEAF
 #define RTZIG_LEAF 2

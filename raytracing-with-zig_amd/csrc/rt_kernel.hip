@@ -264,12 +264,6 @@ __device__ __forceinline__ f2 pk_fma_lo(f2 b, f2 m, f2 a) {
     return r;
 }
 typedef int32_t i2 __attribute__((ext_vector_type(2)));
-typedef int32_t i4v __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ float sel_maskf(float f, float t, uint64_t m) {
-    float r;
-    asm("v_cndmask_b32 %0, %1, %2, %3" : "=v"(r) : "v"(f), "v"(t), "s"(m));
-    return r;
-}
 
 // LDS reads issued as single instructions (the caller waits with s_waitcnt lgkmcnt(0), naming the
 // results as operands so nothing reads them earlier).  `addr` is an LDS byte address.
@@ -277,9 +271,6 @@ template <class T>
 __device__ __forceinline__ void lds_b64(T& v, uint32_t addr, int off) {
     static_assert(sizeof(T) == 8, "b64");
     asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "i"(off));
-}
-__device__ __forceinline__ void lds_b128(i4v& v, uint32_t addr, int off) {
-    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "i"(off));
 }
 __device__ __forceinline__ void lds_b32(int32_t& v, uint32_t addr, int off) {
     asm volatile("ds_read_b32 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "i"(off));
@@ -486,72 +477,6 @@ struct BvhWalker {
             while (cur >= 0) {
                 pr.visit();
                 pr.inner_iter();
-#if RTZIG_BVH4
-                {
-                    // 4-wide step: up to 4 child boxes; descend into the nearest hit child, push the
-                    // other hits (unsorted), pop when none hits
-                    const uint32_t a = (uint32_t)cur;
-                    f2 b[4][3];
-                    i4v refs;
-                    int32_t popped;
-                    if constexpr (kLdsNodes) {
-#pragma unroll
-                        for (int c = 0; c < 4; ++c) {
-                            lds_b64(b[c][0], a + ax, 48 * c);
-                            lds_b64(b[c][1], a + ay, 48 * c);
-                            lds_b64(b[c][2], a + az, 48 * c);
-                        }
-                        lds_b128(refs, a, 192);
-                        lds_b32(popped, lds_addr(top), 0);
-                        asm volatile("s_waitcnt lgkmcnt(0)"
-                                     : "+v"(b[0][0]), "+v"(b[0][1]), "+v"(b[0][2]), "+v"(b[1][0]), "+v"(b[1][1]),
-                                       "+v"(b[1][2]), "+v"(b[2][0]), "+v"(b[2][1]), "+v"(b[2][2]), "+v"(b[3][0]),
-                                       "+v"(b[3][1]), "+v"(b[3][2]), "+v"(refs), "+v"(popped));
-                    } else {
-                        const char* nb = (const char*)nodes + cur;
-#pragma unroll
-                        for (int c = 0; c < 4; ++c) {
-                            b[c][0] = *(const f2*)(nb + 48 * c + ax);
-                            b[c][1] = *(const f2*)(nb + 48 * c + ay);
-                            b[c][2] = *(const f2*)(nb + 48 * c + az);
-                        }
-                        refs = *(const i4v*)(nb + 192);
-                        popped = *top;
-                    }
-                    float nn[4];
-                    uint64_t hm[4];
-#pragma unroll
-                    for (int c = 0; c < 4; ++c) {
-                        const f2 tx = pk_fma_lo(b[c][0], inv_x, noi_x);
-                        const f2 ty = pk_fma_lo(b[c][1], inv_y, noi_y);
-                        const f2 tz = pk_fma_lo(b[c][2], inv_z, noi_z);
-                        nn[c] = slab_near(tx.x, ty.x, tz.x, lower);
-                        const float ff = slab_far(tx.y, ty.y, tz.y, upper);
-                        hm[c] = __ballot(nn[c] <= ff);
-                    }
-                    const float inf = __builtin_inff();
-                    const float k0 = sel_maskf(inf, nn[0], hm[0]), k1 = sel_maskf(inf, nn[1], hm[1]);
-                    const float k2 = sel_maskf(inf, nn[2], hm[2]), k3 = sel_maskf(inf, nn[3], hm[3]);
-                    const uint64_t m01 = __ballot(k1 < k0), m23 = __ballot(k3 < k2);
-                    const float k01 = sel_maskf(k0, k1, m01), k23 = sel_maskf(k2, k3, m23);
-                    const uint64_t mf = __ballot(k23 < k01);
-                    const int32_t rn = sel_mask(sel_mask(refs.x, refs.y, m01), sel_mask(refs.z, refs.w, m23), mf);
-                    const uint64_t any = hm[0] | hm[1] | hm[2] | hm[3];
-                    const uint64_t p0 = hm[0] & (m01 | mf), p1 = hm[1] & (~m01 | mf);
-                    const uint64_t p2 = hm[2] & (m23 | ~mf), p3 = hm[3] & (~m23 | ~mf);
-                    top[kBlockBvh] = refs.x;
-                    top += sel_mask(0, kBlockBvh, p0);
-                    top[kBlockBvh] = refs.y;
-                    top += sel_mask(0, kBlockBvh, p1);
-                    top[kBlockBvh] = refs.z;
-                    top += sel_mask(0, kBlockBvh, p2);
-                    top[kBlockBvh] = refs.w;
-                    top += sel_mask(0, kBlockBvh, p3);
-                    cur = sel_mask(popped, rn, any);
-                    top += sel_mask(-kBlockBvh, 0, any);
-                    continue;
-                }
-#endif
                 f2 bx0, by0, bz0, bx1, by1, bz1;
                 int32_t ref0, ref1, popped;
                 if constexpr (kLdsNodes) {
@@ -1165,11 +1090,11 @@ extern "C" hipError_t rtk_launch_samples_bvh(const rtk::KernelParams* p, const r
     using namespace rtk;
     const uint64_t total = (uint64_t)p->n_rows * p->width * p->s_count;
     if (total == 0) return hipSuccess;
-    if (b->stack_depth < 2 || b->stack_depth > (uint32_t)kMaxStackBvh) return hipErrorInvalidValue;
+    if (b->stack_depth < 2 || b->stack_depth > (uint32_t)kMaxDepthBvh) return hipErrorInvalidValue;
     const size_t stack_bytes = (size_t)b->stack_depth * kBlockBvh * sizeof(int32_t);
     const size_t scene_bytes = (size_t)bvh_leaves_offset(b->n_nodes) + (size_t)b->n_leaves * sizeof(BvhLeaf);
-    // scene in LDS when 16 waves per CU (two 512-thread blocks) still fit a CU's 160 KiB
-    const bool lds_scene = stack_bytes + scene_bytes <= kLdsBudgetBvh;
+    // scene in LDS when two blocks (16 waves) still fit a CU's 160 KiB
+    const bool lds_scene = stack_bytes + scene_bytes <= 80 * 1024;
     const size_t shmem = stack_bytes + (lds_scene ? scene_bytes : 0);
     const uint64_t need = (total + kBlockBvh - 1) / kBlockBvh;
     auto* st = (unsigned long long*)stats;

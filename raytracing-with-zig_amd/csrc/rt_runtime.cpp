@@ -21,7 +21,6 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
-#include <functional>
 #include <limits>
 #include <mutex>
 #include <string>
@@ -224,82 +223,6 @@ void build_bvh(SceneData& sd, double bound) {
     sd.n_leaves = (uint32_t)nl;
     sd.n_always = (uint32_t)na;
     sd.depth = (uint32_t)std::max(2, std::min(bvh.depth, rtk::kMaxDepthBvh));
-#if RTZIG_BVH4
-    // EXPERIMENT: collapse the binary tree into 4-wide nodes (expand the largest-area internal
-    // child until 4 children), empty slots -> a sentinel leaf appended after the real ones
-    struct Ch { float lo[3], hi[3]; int32_t ref; };
-    auto kids = [&](int32_t n) {
-        const rtbvh::Node& s = bvh.nodes[n];
-        std::vector<Ch> v(2);
-        for (int a = 0; a < 3; a++) {
-            v[0].lo[a] = s.lo0[a]; v[0].hi[a] = s.hi0[a];
-            v[1].lo[a] = s.lo1[a]; v[1].hi[a] = s.hi1[a];
-        }
-        v[0].ref = s.ref0;
-        v[1].ref = s.ref1;
-        return v;
-    };
-    auto area = [](const Ch& c) {
-        const double x = c.hi[0] - c.lo[0], y = c.hi[1] - c.lo[1], z = c.hi[2] - c.lo[2];
-        return x * y + y * z + z * x;
-    };
-    std::vector<rtk::BvhNode4> n4;
-    const int32_t empty_ref = ~(int32_t)(nl * sizeof(rtk::BvhLeaf));
-    int max_stack = 0;
-    std::function<int32_t(int32_t, int)> make = [&](int32_t n, int stack) -> int32_t {
-        std::vector<Ch> ch = kids(n);
-        while (ch.size() < 4) {
-            int best = -1;
-            for (int c = 0; c < (int)ch.size(); c++)
-                if (ch[c].ref >= 0 && (best < 0 || area(ch[c]) > area(ch[best]))) best = c;
-            if (best < 0) break;
-            std::vector<Ch> g = kids(ch[best].ref);
-            ch.erase(ch.begin() + best);
-            ch.insert(ch.end(), g.begin(), g.end());
-        }
-        const int32_t idx = (int32_t)n4.size();
-        n4.emplace_back();
-        const int pushed = stack + (int)ch.size() - 1;
-        max_stack = std::max(max_stack, pushed);
-        for (int c = 0; c < 4; c++) {
-            rtk::BvhNode4 tmp = n4[idx];
-            if (c < (int)ch.size()) {
-                for (int a = 0; a < 3; a++) {
-                    tmp.c[c][a][0] = tmp.c[c][a][3] = ch[c].lo[a];
-                    tmp.c[c][a][1] = tmp.c[c][a][2] = ch[c].hi[a];
-                }
-                tmp.ref[c] = ch[c].ref < 0 ? device_ref(ch[c].ref) : 0;
-            } else {
-                for (int a = 0; a < 3; a++) {
-                    tmp.c[c][a][0] = tmp.c[c][a][3] = std::numeric_limits<float>::infinity();
-                    tmp.c[c][a][1] = tmp.c[c][a][2] = -std::numeric_limits<float>::infinity();
-                }
-                tmp.ref[c] = empty_ref;
-            }
-            n4[idx] = tmp;
-        }
-        for (int c = 0; c < (int)ch.size(); c++)
-            if (ch[c].ref >= 0) {
-                const int32_t k = make(ch[c].ref, pushed);
-                n4[idx].ref[c] = k * (int32_t)sizeof(rtk::BvhNode4);
-            }
-        return idx;
-    };
-    make(0, 0);
-    static_assert(sizeof(rtk::BvhNode4) == 2 * sizeof(rtk::BvhNode), "node4 = two node slots");
-    sd.nodes.assign(2 * n4.size(), rtk::BvhNode{});
-    std::memcpy(sd.nodes.data(), n4.data(), n4.size() * sizeof(rtk::BvhNode4));
-    sd.n_nodes = (uint32_t)(2 * n4.size());
-    sd.leaves.resize(nl + 1);  // the sentinel leaf of the empty slots
-    for (int u = 0; u < rtk::kLeafBvh; u++) {
-        const rtk::GeoRec g = geo_of(nullptr);
-        sd.leaves[nl].g[u] = rtk::LeafGeo{g.cx, g.cy, g.cz, g.r2};
-        sd.leaves[nl].sid[u] = rtbvh::kSentinel;
-    }
-    sd.n_leaves = (uint32_t)(nl + 1);
-    sd.depth = (uint32_t)std::max(2, max_stack + 2);
-    if (sd.depth > (uint32_t)rtk::kMaxStackBvh) sd.bvh_ok = false;
-#endif
 }
 
 // Device records + BVH of a sphere list (validated by the caller).
