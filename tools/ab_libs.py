@@ -87,8 +87,10 @@ for rnd in range(args.rounds + 1):
         img = out.cpu()
         if ref is None:
             ref = img
-        if not args.no_check:
-            assert torch.equal(img, ref), f"{path} output differs"
+        if not args.no_check and not torch.equal(img, ref):
+            d = (img != ref).any(dim=-1)
+            idx = d.nonzero()[:8].tolist()
+            raise AssertionError(f"{path} output differs in {int(d.sum())} pixels, e.g. (row, col) {idx}")
         if rnd > 0:
             times[path].append(a.value)
             rtimes[path].append(b.value)
