@@ -144,10 +144,10 @@ int rt_context_sync(rt_context* ctx);
 int rt_context_set_precision(rt_context* ctx, int precision);
 /* Name of the kernel variant the context launches (for profiling / logs). */
 const char* rt_kernel_name(rt_context* ctx);
-/* Optional kernel timing with HIP events recorded on the launch stream around the sample kernel of
- * every render call.  rt_context_kernel_times waits for the last event and returns the duration
- * (ms) of the most recent rt_render_rows_async call; *reduce_ms is 0 (there is no reduce pass since
- * ABI 3: the sample kernel accumulates in sample order itself). */
+/* Optional kernel timing with HIP events recorded on the launch stream around the kernels of every
+ * render call.  rt_context_kernel_times waits for the last event and returns the durations (ms) of
+ * the most recent rt_render_rows_async call: the sample kernel, and the reduce pass of direct mode
+ * (small launches, see rt_render; ~0 when the sample kernel accumulated in order itself). */
 int rt_context_enable_timing(rt_context* ctx, int enable);
 int rt_context_kernel_times(rt_context* ctx, double* sample_ms, double* reduce_ms);
 /* The same summed over every call since timing was (re)enabled (at most 1024 calls; beyond that the
