@@ -27,7 +27,15 @@ SIMDS = 1024
 
 
 def timed(name):
-    return "sample_kernel" in name and not name.split("(")[0].endswith("true>")
+    """The timed parity sample kernel: not the instrumented (kProf) instantiation, not fast mode.
+    Template arguments: sample_kernel_bvh<kLdsScene, kProf, kDirect>,
+    sample_kernel<kLds, U, kWaves, kProf, kDirect>."""
+    head = name.split("(")[0]
+    if "sample_kernel" not in head or "fast" in head or "<" not in head:
+        return False
+    args = [a.strip() for a in head[head.index("<") + 1:head.rindex(">")].split(",")]
+    prof = args[1] if "sample_kernel_bvh<" in head else (args[3] if len(args) > 3 else "false")
+    return prof != "true"
 
 
 def main(tag, workload):
