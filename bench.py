@@ -251,7 +251,9 @@ def main():
         exec_tf = exec_flops / k_frame_s / 1e12
         alg_eq_tf = FLOPS_PER_TEST * n_spheres * rays_per_frame / k_frame_s / 1e12
         issue = None
-        if pmc.get("valu_issue_cycles_per_frame") and pmc.get("clock_GHz"):
+        # the PMC passes profile the whole 1-GPU frame: at N > 1 a rank renders 1/N of it, so the
+        # issue fraction is only reported for the 1-GPU line
+        if world == 1 and pmc.get("valu_issue_cycles_per_frame") and pmc.get("clock_GHz"):
             cyc = pmc["valu_issue_cycles_per_frame"]
             issue = {"frac": round(cyc / (SIMDS * pmc["clock_GHz"] * 1e9 * k_frame_s), 4),
                      "valu_issue_cycles_per_frame": cyc, "clock_GHz": pmc["clock_GHz"],
