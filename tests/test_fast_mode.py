@@ -43,8 +43,11 @@ def check_stat(cam):
     return floor, err
 
 
-def test_fast_final_scene_statistical():
-    """Final random-sphere scene (485 spheres, defocus, all three materials)."""
+@pytest.mark.parametrize("mode", ["ring", "direct"])
+def test_fast_final_scene_statistical(mode, monkeypatch):
+    """Final random-sphere scene (485 spheres, defocus, all three materials), in both unit modes
+    (rt_kernel.h "Work units"; direct is the default at this size)."""
+    monkeypatch.setenv("RTZIG_UNIT_MODE", mode)
     check_stat(rtzig.final_scene_camera(width=480, aspect_ratio=1.5, spp=64))
 
 
@@ -72,8 +75,11 @@ def test_fast_vs_reference_golden(golden_dir):
     assert rmse(a, b) <= 2.0
 
 
-def test_fast_counts_deterministic_and_row_invariant():
-    """Every sample is written once; the image does not depend on the row partition."""
+@pytest.mark.parametrize("mode", ["ring", "direct"])
+def test_fast_counts_deterministic_and_row_invariant(mode, monkeypatch):
+    """Every sample is written once; the image does not depend on the row partition or on the unit
+    mode (both add each pixel's samples in sample order)."""
+    monkeypatch.setenv("RTZIG_UNIT_MODE", mode)
     cam = rtzig.final_scene_camera(width=240, aspect_ratio=1.5, spp=16)
     H, W = cam.height, cam.width
     r = rtzig.DeviceRenderer(0)
@@ -99,4 +105,10 @@ def test_fast_counts_deterministic_and_row_invariant():
     for rank in range(3):
         assert torch.equal(full[rank::3], parts[rank])
     assert torch.isfinite(full).all()
+    other = "direct" if mode == "ring" else "ring"
+    monkeypatch.setenv("RTZIG_UNIT_MODE", other)
+    again2 = torch.zeros_like(full)
+    r.render_rows_async(cam.cam, again2.data_ptr())
+    torch.cuda.synchronize()
+    assert torch.equal(full, again2)
     r.close()
