@@ -34,8 +34,8 @@ constexpr uint32_t kMaxLdsSpheres = 2048;  // 64 KiB of LDS geometry; above this
 // t = s * P + q, and split into kSegs contiguous queue segments with a counter each; a wave claims a
 // run from its home segment with one atomic (guided: 1/8 of an even share of what the segment has
 // left, 64 to 2048 items), then from the other segments 64 at a time; a lane stores its color at
-// samples[t], and nothing waits on anything;
-// reduce_kernel then adds every pixel's stored colors in sample order.  Small launches have few
+// samples[t], and nothing waits on anything; reduce_kernel then adds every pixel's stored colors
+// in sample order.  Small launches have few
 // tiles: (tile, chunk) units would either be large (a long drain) or so many that the claim
 // counter's rate (≈88 claims per µs) bounds the launch.
 // ------------------------------------------------------------------------------------------------
@@ -102,10 +102,9 @@ struct alignas(16) MatRec {
     uint32_t pad;
 };
 
-// Arguments of the sample kernel (by value).  One launch renders the samples
-// [s_begin, s_begin + s_count) of the rows j = row0 + k*row_step, k < n_rows.
-// Work item t in [0, s_count * n_rows * W): sample s_begin + t / P of local pixel q = t % P
-// (P = n_rows * W); its color goes to samples[3*t .. 3*t+2].
+// Arguments of the sample kernel (by value).  One launch renders every sample of the rows
+// j = row0 + k*row_step, k < n_rows (P = n_rows * W launch-local pixels q, row k = q / W); the
+// work decomposition (units or direct items) is UnitArgs's.
 struct KernelParams {
     uint32_t width, height, spp, bounce_max;
     double scale;  // pixelSamplesScale
