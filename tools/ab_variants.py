@@ -1,8 +1,9 @@
 #!/usr/bin/env python3
 """A/B the sample-kernel variants IN ONE PROCESS, interleaved rounds (cdna guide rule 24).
 
-    RTZIG_VARIANTS="1 2 4" python tools/ab_variants.py --spp 100 --rounds 5
-Each variant is selected through the --env variable (default RTZIG_UNROLL), set both while the
+    python tools/ab_variants.py --spp 100 --rounds 5                 # the walk variants
+    python tools/ab_variants.py --env RTZIG_UNIT_MODE --variants "ring direct"
+Each variant is selected through the --env variable (default RTZIG_KERNEL), set both while the
 variant's scene is built and at every launch.  Prints one JSON line with
 per-variant median/min sample-kernel ms (HIP events) and Msamples/s.
 """
@@ -23,8 +24,8 @@ ap.add_argument("--width", type=int, default=1200)
 ap.add_argument("--aspect", type=float, default=1.5)
 ap.add_argument("--spp", type=int, default=100)
 ap.add_argument("--rounds", type=int, default=5)
-ap.add_argument("--env", default="RTZIG_UNROLL")
-ap.add_argument("--variants", default=os.environ.get("RTZIG_VARIANTS", "1 2 4"))
+ap.add_argument("--env", default="RTZIG_KERNEL")
+ap.add_argument("--variants", default=os.environ.get("RTZIG_VARIANTS", "bvh smem_u4 lds_u4"))
 args = ap.parse_args()
 
 cam = rtzig.final_scene_camera(width=args.width, aspect_ratio=args.aspect, spp=args.spp)
