@@ -30,8 +30,10 @@ __device__ __forceinline__ void st_wt(double* p, double v) {  // global_store_dw
 }
 
 // A wave that cannot claim and has nothing to trace sleeps between polls; a bug that broke the
-// dependency chain would otherwise hang the GPU, so the wait is bounded (≈ 0.5 s of sleeping per
-// wave): past it the wave reports it in ctr[kErrWord] and gives up (the host returns RT_ERR_HIP).
+// dependency chain would otherwise hang the GPU, so each continuous wait is bounded (≈ 0.5 s of
+// sleeping; the count restarts whenever the wave finalises or claims a unit, so a long launch's
+// many short waits never add up to it): past it the wave reports it in ctr[kErrWord] and gives up
+// (the host returns RT_ERR_HIP).
 constexpr uint32_t kSpinLimit = 1u << 22;
 
 
@@ -46,7 +48,8 @@ struct UnitSched {
     uint32_t cur_slot = 0, cur = 0, end = 0;  // the slot being handed out: items [cur, end)
     uint32_t cur_tile = 0, cur_s0 = 0;
     uint32_t st_u[kSlots];           // unit id held by each slot
-    uint32_t spins = 0;
+    uint32_t spins = 0;              // sleeps in all (diagnostics)
+    uint32_t wait_run = 0;           // sleeps since the last finalisation or claim
     uint32_t seen = 0;               // direct mode: item position after this wave's last claim
     uint32_t waves = 1;              // direct mode: the launch's waves
     uint32_t seg = 0, empty = 0;     // direct mode: segment claimed from; segments found empty
@@ -87,6 +90,7 @@ struct UnitSched {
                 if (lane == 0) t = (uint32_t)atomicAdd(ua.ctr + kCtrStride * seg, (unsigned long long)k);
                 t = lo + __builtin_amdgcn_readfirstlane(t);
                 if (t < hi) {
+                    wait_run = 0;
                     seen = t + k;
                     cur = t;
                     end = hi - t < k ? hi : t + k;
@@ -120,6 +124,7 @@ struct UnitSched {
         for (uint32_t j = 0; j < kSlots; ++j) st_u[j] = j == js ? u : st_u[j];
         busy |= 1u << js;
         cur_slot = js;
+        wait_run = 0;
         cur = 0;
         end = n * 64;
         cur_tile = tile;
@@ -248,6 +253,7 @@ struct UnitSched {
             if (lane == 0 && k + 1 < ua.n_chunks)
                 __hip_atomic_store((gu32*)ua.flags + tile, k + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             busy &= ~(1u << j);
+            wait_run = 0;
             return true;
         }
         return false;
@@ -255,7 +261,8 @@ struct UnitSched {
 
     // Nothing to trace in this wave: wait for a dependency (bounded).  False: give up (reported).
     __device__ __forceinline__ bool wait(uint32_t lane) {
-        if (++spins > kSpinLimit) {
+        ++spins;
+        if (++wait_run > kSpinLimit) {
             if (lane == 0) atomicOr(ua.ctr + kErrWord, 1ull);
             failed = true;
             return false;

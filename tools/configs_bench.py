@@ -53,6 +53,7 @@ for name, cam in configs:
                             "ms_per_frame": round(ms, 3), "Msamples_s": round(W * H * spp / ms / 1e3, 1),
                             "rays_per_sample": round(rays / (W * H * spp), 4)}
     print(name, res["configs"][name], file=sys.stderr, flush=True)
+    r.sync()  # raises if a wave reported a hand-off timeout
     r.close()
 print(json.dumps(res))
 if args.out:
