@@ -24,9 +24,10 @@ def _free_port():
     return p
 
 
-def _rank(rank, world, port, q):
+def _rank(rank, world, port, q, mode):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
+    os.environ["RTZIG_UNIT_MODE"] = mode
     import torch
     import torch.distributed as dist
 
@@ -54,13 +55,16 @@ def _rank(rank, world, port, q):
         dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("mode", ["ring", "direct"])
 @pytest.mark.parametrize("world", [2, 3])
-def test_hip_ranks_gather_equals_single_rank(oracle, world):
+def test_hip_ranks_gather_equals_single_rank(oracle, world, mode):
+    """Both unit modes on every rank (ring: in-kernel ordered accumulation; direct: stored samples
+    + reduce pass, the mode a rank's rows of an 8-GPU job use)."""
     import rtzig
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_rank, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_rank, args=(r, world, port, q, mode)) for r in range(world)]
     for p in procs:
         p.start()
     try:
