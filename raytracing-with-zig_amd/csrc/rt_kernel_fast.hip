@@ -328,7 +328,9 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
 
     while (true) {
         // ---- finalise one unit whose samples have all ended (rt_units.h) --------------------------
+        __builtin_amdgcn_s_setprio(2);
         const bool progressed = us.finalize_one(us.ready_mask(active, myslot), lane);
+        __builtin_amdgcn_s_setprio(0);
         // ---- refill (as the parity kernel's path_loop) -----------------------------------------
         bool fresh = false;
         uint32_t fq = 0, fs = 0;
@@ -407,7 +409,9 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
             } else {
                 float t;
                 ++rays;
+                __builtin_amdgcn_s_setprio(2);  // as the parity kernel (rt_kernel.hip, path_loop)
                 const int k = walk(r, t_min, t_max, &t);
+                __builtin_amdgcn_s_setprio(0);
                 MatRec m{};
                 f3 pt = mk(0, 0, 0), nrm = mk(0, 0, 0);
                 bool front = false;
