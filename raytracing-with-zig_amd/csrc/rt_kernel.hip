@@ -750,11 +750,12 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
                 if constexpr (kProf) { v0 = pr.n_visits; t0 = pr.n_tests; }
                 // The walk is a chain of dependent LDS reads: raised issue priority lets a wave whose
                 // node data has arrived issue its next step ahead of the co-resident waves' shading
-                // and sampling work (-0.8% kernel time; the finalisation below likewise, -0.2%; a
-                // raised priority everywhere but the trip loop was slower)
+                // and sampling work (-0.8% kernel time; the finalisation above likewise, -0.2%; a
+                // raised priority everywhere but the trip loop was slower).  The shading that follows
+                // (dependent loads of the hit sphere's records) runs at priority 1 (chapter 13 -1.3%).
                 __builtin_amdgcn_s_setprio(2);
                 const int k = walk(r, p.t_min, p.t_max, &t, pr);
-                __builtin_amdgcn_s_setprio(0);
+                __builtin_amdgcn_s_setprio(1);
                 if constexpr (kProf) {
                     if (bounce == 0) { pr.cam_visits += pr.n_visits - v0; pr.cam_tests += pr.n_tests - t0; }
                 }
@@ -823,6 +824,7 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
                 }
             }
         }
+        __builtin_amdgcn_s_setprio(0);
         if (done) {
             us.store(myslot, mi, col.x, col.y, col.z);
             ++nsamples;
