@@ -30,6 +30,7 @@ struct Prim {
 };
 
 struct Builder {
+    const std::vector<TrainRay>* train = nullptr;
     std::vector<Prim> prims;
     std::vector<Node> nodes;
     std::vector<uint32_t> slots;  // leaf slots (after the always-list)
@@ -80,8 +81,83 @@ struct Builder {
         return ~(int32_t)index;
     }
 
-    // returns the ref of the subtree over prims[b, e) at `depth` (root = 1)
-    int32_t build(size_t b, size_t e, int depth) {
+    // does the sample segment [t_min, tmax] of ray `r` enter the box?  (f64 slabs; a zero direction
+    // component tests the origin against that slab)
+    static bool seg_hits(const TrainRay& r, const double lo[3], const double hi[3]) {
+        double t0 = 1e-3, t1 = r.tmax;
+        for (int a = 0; a < 3; a++) {
+            if (r.d[a] == 0) {
+                if (r.o[a] < lo[a] || r.o[a] > hi[a]) return false;
+                continue;
+            }
+            const double inv = 1.0 / r.d[a];
+            double ta = (lo[a] - r.o[a]) * inv, tb = (hi[a] - r.o[a]) * inv;
+            if (ta > tb) std::swap(ta, tb);
+            t0 = std::max(t0, ta);
+            t1 = std::min(t1, tb);
+        }
+        return t0 <= t1;
+    }
+
+    // Ray-driven split cost over prims[b, e) sorted on one axis, for every split i (left = first i):
+    // cost[i] = (segments entering the left box) * i^e + (segments entering the right box) * (n - i)^e
+    // with e = kRayCostExp: the work a segment does below a box it enters grows with the box's
+    // sphere count, but (a near-first walk stops early) much slower than linearly.
+    // The left boxes grow with i and the right boxes shrink, so each segment's first entering left
+    // split and last entering right split are found by bisection.
+    void ray_costs(size_t b, size_t e, const std::vector<uint32_t>& rays, std::vector<double>& cost) const {
+        const size_t n = e - b;
+        std::vector<double> L(6 * n), R(6 * n);  // L[i]: box of the first i prims, R[i]: of prims i..n-1
+        double lo[3], hi[3];
+        for (int a = 0; a < 3; a++) { lo[a] = prims[b].lo[a]; hi[a] = prims[b].hi[a]; }
+        for (size_t i = 1; i < n; i++) {
+            for (int a = 0; a < 3; a++) { L[6 * i + a] = lo[a]; L[6 * i + 3 + a] = hi[a]; }
+            for (int a = 0; a < 3; a++) {
+                lo[a] = std::min(lo[a], prims[b + i].lo[a]);
+                hi[a] = std::max(hi[a], prims[b + i].hi[a]);
+            }
+        }
+        for (int a = 0; a < 3; a++) { lo[a] = prims[e - 1].lo[a]; hi[a] = prims[e - 1].hi[a]; }
+        for (size_t i = n - 1; i >= 1; i--) {
+            for (int a = 0; a < 3; a++) { R[6 * i + a] = lo[a]; R[6 * i + 3 + a] = hi[a]; }
+            for (int a = 0; a < 3; a++) {
+                lo[a] = std::min(lo[a], prims[b + i - 1].lo[a]);
+                hi[a] = std::max(hi[a], prims[b + i - 1].hi[a]);
+            }
+        }
+        std::vector<double> first_l(n + 1, 0.0), last_r(n + 1, 0.0);  // histograms
+        for (uint32_t ri : rays) {
+            const TrainRay& r = (*train)[ri];
+            if (seg_hits(r, &L[6 * (n - 1)], &L[6 * (n - 1) + 3])) {
+                size_t l = 1, h = n - 1;  // smallest i with a hit
+                while (l < h) {
+                    const size_t m = (l + h) / 2;
+                    if (seg_hits(r, &L[6 * m], &L[6 * m + 3])) h = m; else l = m + 1;
+                }
+                first_l[l] += 1;
+            }
+            if (seg_hits(r, &R[6], &R[9])) {
+                size_t l = 1, h = n - 1;  // largest i with a hit
+                while (l < h) {
+                    const size_t m = (l + h + 1) / 2;
+                    if (seg_hits(r, &R[6 * m], &R[6 * m + 3])) l = m; else h = m - 1;
+                }
+                last_r[l] += 1;
+            }
+        }
+        cost.assign(n, std::numeric_limits<double>::infinity());
+        double hl = 0, hr = 0;
+        std::vector<double> hits_r(n + 1, 0.0);
+        for (size_t i = n - 1; i >= 1; i--) { hr += last_r[i]; hits_r[i] = hr; }
+        for (size_t i = 1; i < n; i++) {
+            hl += first_l[i];
+            cost[i] = hl * std::pow((double)i, kRayCostExp) + hits_r[i] * std::pow((double)(n - i), kRayCostExp);
+        }
+    }
+
+    // returns the ref of the subtree over prims[b, e) at `depth` (root = 1); `rays`: the sample
+    // segments that enter this subtree's box
+    int32_t build(size_t b, size_t e, int depth, const std::vector<uint32_t>& rays = {}) {
         max_depth = std::max(max_depth, depth);
         const size_t n = e - b;
         if (n <= (size_t)kLeafMax) return leaf(b, e);
@@ -109,6 +185,17 @@ struct Builder {
                     best_axis = ax;
                     best_split = b + n / 2;
                 }
+                continue;
+            }
+            if (train && rays.size() >= kMinTrain) {
+                std::vector<double> cost;
+                ray_costs(b, e, rays, cost);
+                for (size_t i = 1; i < n; i++)
+                    if (cost[i] < best_cost) {
+                        best_cost = cost[i];
+                        best_axis = ax;
+                        best_split = b + i;
+                    }
                 continue;
             }
             double lo[3], hi[3];
@@ -140,8 +227,18 @@ struct Builder {
         });
         const size_t me = nodes.size();
         nodes.emplace_back();
-        const int32_t r0 = build(b, best_split, depth + 1);
-        const int32_t r1 = build(best_split, e, depth + 1);
+        std::vector<uint32_t> rays0, rays1;
+        if (train && rays.size() >= kMinTrain) {
+            double lo[3], hi[3];
+            bounds(b, best_split, lo, hi);
+            for (uint32_t ri : rays)
+                if (seg_hits((*train)[ri], lo, hi)) rays0.push_back(ri);
+            bounds(best_split, e, lo, hi);
+            for (uint32_t ri : rays)
+                if (seg_hits((*train)[ri], lo, hi)) rays1.push_back(ri);
+        }
+        const int32_t r0 = build(b, best_split, depth + 1, rays0);
+        const int32_t r1 = build(best_split, e, depth + 1, rays1);
         Node& nd = nodes[me];
         set_box(nd.lo0, nd.hi0, b, best_split);
         set_box(nd.lo1, nd.hi1, best_split, e);
@@ -174,10 +271,11 @@ double scene_extent(const rt_sphere* s, size_t n) {
     return m;
 }
 
-Bvh build(const rt_sphere* spheres, size_t n, double origin_bound) {
+Bvh build(const rt_sphere* spheres, size_t n, double origin_bound, const std::vector<TrainRay>* train) {
     Bvh out;
     out.origin_bound = origin_bound;
     Builder B;
+    B.train = train;
     std::vector<uint32_t> always;
     const double e_origin = std::ldexp(origin_bound, -21);
     for (size_t k = 0; k < n; k++) {
@@ -252,7 +350,14 @@ Bvh build(const rt_sphere* spheres, size_t n, double origin_bound) {
         nd.pad[0] = nd.pad[1] = 0;
         B.max_depth = 2;
     } else {
-        B.build(0, m, 1);
+        std::vector<uint32_t> rays;
+        if (train) {
+            double lo[3], hi[3];
+            B.bounds(0, m, lo, hi);
+            for (size_t i = 0; i < train->size(); i++)
+                if (Builder::seg_hits((*train)[i], lo, hi)) rays.push_back((uint32_t)i);
+        }
+        B.build(0, m, 1, rays);
     }
     if (B.failed) return out;  // ok = false: the runtime falls back to the linear walk
     out.nodes = std::move(B.nodes);
@@ -261,6 +366,210 @@ Bvh build(const rt_sphere* spheres, size_t n, double origin_bound) {
     out.n_always = (uint32_t)always.size();
     out.depth = B.max_depth;
     out.ok = true;
+    return out;
+}
+
+namespace {
+
+double sphere_root(const rt_sphere& s, const double o[3], const double d[3], double t_min, double closest) {
+    const double r = s.radius > 0 ? s.radius : 0.0;
+    double oc[3], a = 0, h = 0, c = 0;
+    for (int k = 0; k < 3; k++) {
+        oc[k] = s.center[k] - o[k];
+        a += d[k] * d[k];
+        h += d[k] * oc[k];
+        c += oc[k] * oc[k];
+    }
+    c -= r * r;
+    const double disc = h * h - a * c;
+    if (!(disc >= 0)) return std::numeric_limits<double>::infinity();
+    const double sq = std::sqrt(disc);
+    double t = (h - sq) / a;
+    if (!(t_min < t && t < closest)) {
+        t = (h + sq) / a;
+        if (!(t_min < t && t < closest)) return std::numeric_limits<double>::infinity();
+    }
+    return t;
+}
+
+bool box_enter(const float* lo, const float* hi, const double o[3], const double inv[3], double t0, double t1,
+               double* tn) {
+    for (int a = 0; a < 3; a++) {
+        double ta = ((double)lo[a] - o[a]) * inv[a], tb = ((double)hi[a] - o[a]) * inv[a];
+        if (ta > tb) std::swap(ta, tb);
+        if (ta > t0) t0 = ta;  // NaN (0 * inf) keeps the box: permissive
+        if (tb < t1) t1 = tb;
+    }
+    *tn = t0;
+    return t0 <= t1;
+}
+
+// SplitMix64-driven uniform doubles in [0, 1) (training only; not the reference's stream)
+struct TrainRng {
+    uint64_t x;
+    double next() {
+        uint64_t z = (x += 0x9E3779B97F4A7C15ull);
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        return (double)((z ^ (z >> 31)) >> 11) * 0x1p-53;
+    }
+};
+
+}  // namespace
+
+int closest_hit(const Bvh& tree, const rt_sphere* spheres, const double o[3], const double d[3], double t_min,
+                double* t_out) {
+    double closest = std::numeric_limits<double>::infinity();
+    int best = -1;
+    auto test = [&](uint32_t k) {
+        if (k == kSentinel) return;
+        const double t = sphere_root(spheres[k], o, d, t_min, closest);
+        if (t < closest || (t == closest && best >= 0 && (int)k < best)) {
+            closest = t;
+            best = (int)k;
+        }
+    };
+    for (uint32_t q = 0; q < tree.n_always; q++) test(tree.slot_to_sphere[q]);
+    if (!tree.nodes.empty()) {
+        double inv[3];
+        for (int a = 0; a < 3; a++) inv[a] = 1.0 / (d[a] == 0 ? 1e-300 : d[a]);
+        int32_t stack[kMaxDepth + 2];
+        int sp = 0;
+        int32_t cur = 0;
+        while (true) {
+            if (cur >= 0) {
+                const Node& nd = tree.nodes[(size_t)cur];
+                double n0, n1;
+                const bool h0 = box_enter(nd.lo0, nd.hi0, o, inv, t_min, closest, &n0);
+                const bool h1 = box_enter(nd.lo1, nd.hi1, o, inv, t_min, closest, &n1);
+                if (h0 && h1) {
+                    stack[sp++] = n0 <= n1 ? nd.ref1 : nd.ref0;
+                    cur = n0 <= n1 ? nd.ref0 : nd.ref1;
+                    continue;
+                }
+                if (h0 || h1) {
+                    cur = h0 ? nd.ref0 : nd.ref1;
+                    continue;
+                }
+            } else {
+                const size_t base = tree.n_always + (size_t)kLeafMax * (size_t)(~cur);
+                for (int u = 0; u < kLeafMax; u++) test(tree.slot_to_sphere[base + (size_t)u]);
+            }
+            if (sp == 0) break;
+            cur = stack[--sp];
+        }
+    }
+    *t_out = closest;
+    return best;
+}
+
+std::vector<TrainRay> sample_rays(const rt_sphere* spheres, size_t n, const rt_camera& cam, const Bvh& tree,
+                                  size_t n_samples, uint64_t seed) {
+    std::vector<TrainRay> out;
+    if (!tree.ok || n == 0 || cam.image_width == 0 || cam.image_height == 0) return out;
+    TrainRng g{seed};
+    // pixel grid with ~n_samples points, stride s in both directions
+    const double area = (double)cam.image_width * (double)cam.image_height;
+    const uint32_t s = (uint32_t)std::max(1.0, std::floor(std::sqrt(area / (double)std::max<size_t>(n_samples, 1))));
+    const uint32_t bounce_max = std::min<uint32_t>(cam.bounce_max, 50);
+    auto unit_vec = [&](double v[3]) {  // Vec.randomUnitVec (vec.zig:71-80) by rejection
+        while (true) {
+            double l = 0;
+            for (int k = 0; k < 3; k++) {
+                v[k] = 2 * g.next() - 1;
+                l += v[k] * v[k];
+            }
+            if (1e-160 < l && l <= 1) {
+                const double sl = std::sqrt(l);
+                for (int k = 0; k < 3; k++) v[k] /= sl;
+                return;
+            }
+        }
+    };
+    for (uint32_t j = 0; j < cam.image_height; j += s)
+        for (uint32_t i = 0; i < cam.image_width; i += s) {
+            const double pi = (double)i + s * g.next() - 0.5, pj = (double)j + s * g.next() - 0.5;
+            double o[3], d[3];
+            double px = 0, py = 0;
+            if (cam.defocus_angle > 0) {
+                do {
+                    px = 2 * g.next() - 1;
+                    py = 2 * g.next() - 1;
+                } while (px * px + py * py >= 1);
+            }
+            for (int k = 0; k < 3; k++) {
+                const double ps = cam.pixel0[k] + cam.du[k] * pi + cam.dv[k] * pj;
+                o[k] = cam.center[k] + (cam.defocus_angle > 0 ? cam.defocus_disk_u[k] * px + cam.defocus_disk_v[k] * py : 0.0);
+                d[k] = ps - o[k];
+            }
+            for (uint32_t b = 0; b < bounce_max; b++) {
+                double t;
+                const int k = closest_hit(tree, spheres, o, d, cam.t_min, &t);
+                TrainRay r;
+                for (int a = 0; a < 3; a++) {
+                    r.o[a] = o[a];
+                    r.d[a] = d[a];
+                }
+                r.tmax = k >= 0 ? t : std::numeric_limits<double>::infinity();
+                out.push_back(r);
+                if (k < 0) break;
+                const rt_sphere& S = spheres[k];
+                const double rad = S.radius > 0 ? S.radius : 0.0;
+                double p[3], nr[3], dn = 0;
+                for (int a = 0; a < 3; a++) {
+                    p[a] = o[a] + d[a] * t;
+                    nr[a] = (p[a] - S.center[a]) / rad;
+                    dn += d[a] * nr[a];
+                }
+                if (dn >= 0)
+                    for (int a = 0; a < 3; a++) nr[a] = -nr[a];
+                double v[3];
+                if (S.material == RT_LAMBERTIAN) {
+                    unit_vec(v);
+                    for (int a = 0; a < 3; a++) d[a] = nr[a] + v[a];
+                } else if (S.material == RT_METAL) {
+                    double rf[3], l = 0, dd = 0;
+                    for (int a = 0; a < 3; a++) dd += d[a] * nr[a];
+                    for (int a = 0; a < 3; a++) {
+                        rf[a] = d[a] - 2 * dd * nr[a];
+                        l += rf[a] * rf[a];
+                    }
+                    unit_vec(v);
+                    double dot_n = 0;
+                    for (int a = 0; a < 3; a++) {
+                        d[a] = rf[a] / std::sqrt(l) + S.fuzz * v[a];
+                        dot_n += d[a] * nr[a];
+                    }
+                    if (!(dot_n > 0)) break;
+                } else {
+                    const double ri = dn < 0 ? 1.0 / S.refraction_index : S.refraction_index;
+                    double u[3], l = 0, c = 0;
+                    for (int a = 0; a < 3; a++) l += d[a] * d[a];
+                    for (int a = 0; a < 3; a++) {
+                        u[a] = d[a] / std::sqrt(l);
+                        c -= u[a] * nr[a];
+                    }
+                    c = std::min(c, 1.0);
+                    const double sn = std::sqrt(std::max(0.0, 1 - c * c));
+                    double r0 = (1 - ri) / (1 + ri);
+                    r0 *= r0;
+                    if (ri * sn > 1 || r0 + (1 - r0) * std::pow(1 - c, 5) > g.next()) {
+                        double un = 0;
+                        for (int a = 0; a < 3; a++) un += u[a] * nr[a];
+                        for (int a = 0; a < 3; a++) d[a] = u[a] - 2 * un * nr[a];
+                    } else {
+                        double perp[3], pl = 0;
+                        for (int a = 0; a < 3; a++) {
+                            perp[a] = ri * (u[a] + c * nr[a]);
+                            pl += perp[a] * perp[a];
+                        }
+                        const double par = -std::sqrt(std::fabs(1 - pl));
+                        for (int a = 0; a < 3; a++) d[a] = perp[a] + par * nr[a];
+                    }
+                }
+                for (int a = 0; a < 3; a++) o[a] = p[a];
+            }
+        }
     return out;
 }
 

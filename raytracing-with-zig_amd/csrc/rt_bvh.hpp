@@ -26,6 +26,8 @@ constexpr double kAlwaysArea = 0.25;  // box-area fraction above which a sphere 
 constexpr double kAlwaysRel = 10.0;   // ... or box area above this multiple of the median sphere's
 constexpr int kMaxBig = 4;           // at most this many such spheres
 constexpr uint32_t kSentinel = 0xffffffffu;  // slot_to_sphere value of a padding slot
+constexpr size_t kMinTrain = 64;             // ray-driven splits need at least this many segments
+constexpr double kRayCostExp = 0.4;          // ray-driven split cost: segments x spheres^kRayCostExp
 
 // Internal node: the boxes of both children (f32, padded outward) and their refs.
 // ref >= 0: internal node index; ref < 0: leaf index ~ref.  Leaf L holds slots
@@ -47,9 +49,32 @@ struct Bvh {
     bool ok = false;
 };
 
+// A sample ray segment [t_min, tmax] of the workload, for the ray-driven split cost (below).
+struct TrainRay {
+    double o[3], d[3];
+    double tmax;  // the segment's end: its closest hit (or +inf)
+};
+
 // Builds the BVH.  `origin_bound`: bound on |ray origin| components the padding must cover
 // (at least the scene's own extent; the runtime raises it for far-away cameras).
-Bvh build(const rt_sphere* spheres, size_t n, double origin_bound);
+// `train` (optional): sample rays of the workload.  Each split then minimises the number of sample
+// segments that enter each child box times the child's sphere count (the SAH's surface area is the
+// same probability for uniformly distributed lines); nodes reached by fewer than kMinTrain
+// segments use the SAH.
+Bvh build(const rt_sphere* spheres, size_t n, double origin_bound, const std::vector<TrainRay>* train = nullptr);
+
+// Closest hit of the ray (o, d) beyond t_min over the tree: a host traversal in plain f64, used to
+// sample training rays (not the kernel's exact arithmetic).  Returns the sphere index or -1; *t =
+// its root.
+int closest_hit(const Bvh& tree, const rt_sphere* spheres, const double o[3], const double d[3], double t_min,
+                double* t);
+
+// Training segments for the ray-driven build: the paths of about `n_samples` camera samples spread
+// over the whole image (a jittered pixel grid), traced through `tree` with the reference's camera
+// and scatter rules (camera.zig:148-215, material.zig:27-110) and a local generator; every segment
+// with its closest hit.  Deterministic for a given seed.
+std::vector<TrainRay> sample_rays(const rt_sphere* spheres, size_t n, const rt_camera& cam, const Bvh& tree,
+                                  size_t n_samples, uint64_t seed);
 
 // Max |coordinate| of any sphere's bounding box (finite spheres only).
 double scene_extent(const rt_sphere* spheres, size_t n);

@@ -53,7 +53,18 @@ struct SceneData {
     std::vector<rtk::GeoRec> ageo;
     std::vector<uint32_t> asid;
     uint32_t n_nodes = 0, n_leaves = 0, n_always = 0, depth = 0;
+    bool trained = false;  // the tree was built from sample rays of camera `view` (train_bvh)
+    rt_camera view{};
 };
+
+// Ray-driven tree (rtbvh::build with sample rays): trained for launches of at least
+// kTrainMinSamples samples on scenes of at least kTrainMinSpheres spheres, from the paths of
+// kTrainSamples camera samples.  Config 4: node visits per ray 6.97 -> 6.2.
+constexpr uint64_t kTrainMinSamples = 1ull << 25;
+constexpr size_t kTrainMinSpheres = 32;
+constexpr size_t kTrainSamples = 6000;
+constexpr uint64_t kTrainSeed = 0x7261792d74726565ull;
+constexpr size_t kLdsTreeBytes = 80 * 1024;  // rtk_launch_samples_bvh's LDS budget per block
 
 }  // namespace
 
@@ -176,9 +187,9 @@ rtk::GeoRec geo_of(const rt_sphere* s) {
     return g;
 }
 
-// The BVH of sd.spheres, valid for ray origins with |o_i| <= bound (device layout, rt_kernel.h).
-void build_bvh(SceneData& sd, double bound) {
-    const rtbvh::Bvh bvh = rtbvh::build(sd.spheres.data(), sd.spheres.size(), bound);
+// Sets sd's device tree from `bvh` (built for ray origins with |o_i| <= bound; rt_kernel.h layout).
+void set_tree(SceneData& sd, const rtbvh::Bvh& bvh, double bound) {
+    sd.trained = false;
     // byte-offset refs must fit int32 (and stay clear of the walk's INT32_MIN "done" marker)
     const bool fits = bvh.nodes.size() * sizeof(rtk::BvhNode) < (1ull << 30) &&
                       bvh.slot_to_sphere.size() / rtk::kLeafBvh * sizeof(rtk::BvhLeaf) < (1ull << 30);
@@ -223,6 +234,69 @@ void build_bvh(SceneData& sd, double bound) {
     sd.n_leaves = (uint32_t)nl;
     sd.n_always = (uint32_t)na;
     sd.depth = (uint32_t)std::max(2, std::min(bvh.depth, rtk::kMaxDepthBvh));
+}
+
+// The SAH BVH of sd.spheres, valid for ray origins with |o_i| <= bound.
+void build_bvh(SceneData& sd, double bound) {
+    set_tree(sd, rtbvh::build(sd.spheres.data(), sd.spheres.size(), bound), bound);
+}
+
+// Do two cameras shoot the same rays (every field getRay / rayColor read except spp and seed)?
+bool same_view(const rt_camera& a, const rt_camera& b) {
+    rt_camera x = a, y = b;
+    x.samples_per_pixel = y.samples_per_pixel = 0;
+    x.pixel_samples_scale = y.pixel_samples_scale = 0;
+    x.seed = y.seed = 0;
+    return std::memcmp(&x, &y, sizeof x) == 0;
+}
+
+// Should a launch of `samples` samples train the tree for its camera?  RTZIG_BVH_TRAIN=0|1 forces
+// it off / on (test hook: trained trees on small launches).
+bool want_train(const SceneData& sd, uint64_t samples) {
+    if (const char* e = std::getenv("RTZIG_BVH_TRAIN")) {
+        if (std::strcmp(e, "0") == 0) return false;
+        if (std::strcmp(e, "1") == 0) return sd.bvh_ok;
+    }
+    return sd.bvh_ok && samples >= kTrainMinSamples && sd.spheres.size() >= kTrainMinSpheres;
+}
+
+// Rebuilds sd's tree from sample rays of `cam` (rtbvh::sample_rays over the SAH tree, then the
+// ray-driven build).  The result depends only on (spheres, origin bound, view), so it is memoised
+// process-wide: rt_render's devices and later calls reuse it.  Any valid tree returns the same
+// bits (rt_bvh.hpp); this one only visits fewer nodes for this camera's rays.
+void train_bvh(SceneData& sd, const rt_camera& cam) {
+    static std::mutex mu;
+    static SceneData memo;
+    std::lock_guard<std::mutex> lock(mu);
+    if (memo.trained && same_view(memo.view, cam) && memo.origin_bound == sd.origin_bound &&
+        memo.spheres.size() == sd.spheres.size() &&
+        std::memcmp(memo.spheres.data(), sd.spheres.data(), sd.spheres.size() * sizeof(rt_sphere)) == 0) {
+        sd = memo;
+        return;
+    }
+    const double bound = sd.origin_bound;
+    const rtbvh::Bvh sah = rtbvh::build(sd.spheres.data(), sd.spheres.size(), bound);
+    if (!sah.ok) return;
+    const std::vector<rtbvh::TrainRay> rays =
+        rtbvh::sample_rays(sd.spheres.data(), sd.spheres.size(), cam, sah, kTrainSamples, kTrainSeed);
+    const rtbvh::Bvh tree = rtbvh::build(sd.spheres.data(), sd.spheres.size(), bound, &rays);
+    if (!tree.ok) return;
+    // the kernel stages the tree in LDS when tree + stacks fit a block's 80 KiB (rt_kernel.hip); a
+    // trained tree that would not fit where the SAH tree does (or does not build) is not used
+    auto lds_bytes = [](const SceneData& t) {
+        return (size_t)rtk::bvh_leaves_offset(t.n_nodes) + (size_t)t.n_leaves * sizeof(rtk::BvhLeaf) +
+               (size_t)t.depth * rtk::kBlockBvh * sizeof(int32_t);
+    };
+    SceneData sah_sd = sd;
+    set_tree(sah_sd, sah, bound);
+    set_tree(sd, tree, bound);
+    if (!sd.bvh_ok || (lds_bytes(sd) > kLdsTreeBytes && lds_bytes(sah_sd) <= kLdsTreeBytes)) {
+        sd = sah_sd;
+        return;
+    }
+    sd.trained = true;
+    sd.view = cam;
+    memo = sd;
 }
 
 // Device records + BVH of a sphere list (validated by the caller).
@@ -511,6 +585,15 @@ int rt_render_rows_async(rt_context* ctx, const rt_camera* cam, uint32_t output_
         rc = quiesce(ctx);  // the previous render may still walk the old tree
         if (rc) return rc;
         build_bvh(ctx->scene, std::max(cam_bound, ctx->scene.origin_bound) * 1.01);
+        rc = upload_bvh(ctx);
+        if (rc) return rc;
+    }
+    // large launches walk a tree trained on this camera's rays (same bits, fewer node visits)
+    if (want_train(ctx->scene, (uint64_t)n_rows * cam->image_width * cam->samples_per_pixel) &&
+        !(ctx->scene.trained && same_view(ctx->scene.view, *cam))) {
+        rc = quiesce(ctx);  // the previous render may still walk the old tree
+        if (rc) return rc;
+        train_bvh(ctx->scene, *cam);
         rc = upload_bvh(ctx);
         if (rc) return rc;
     }

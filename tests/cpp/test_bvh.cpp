@@ -57,9 +57,36 @@ static void check_boxes(const rtbvh::Bvh& b, const std::vector<rt_sphere>& s, in
     }
 }
 
-static void run(const std::vector<rt_sphere>& s, const char* name) {
-    const double ext = rtbvh::scene_extent(s.data(), s.size());
-    const rtbvh::Bvh b = rtbvh::build(s.data(), s.size(), ext);
+// a pinhole camera at `from` looking at the origin, 160x90 pixels (training-ray sampler input)
+static rt_camera look_at(double fx, double fy, double fz) {
+    rt_camera c{};
+    c.image_width = 160; c.image_height = 90; c.samples_per_pixel = 1; c.bounce_max = 50;
+    const double f[3] = {fx, fy, fz};
+    double w[3], l = std::sqrt(fx * fx + fy * fy + fz * fz);
+    for (int a = 0; a < 3; a++) w[a] = f[a] / l;
+    double u[3] = {w[2], 0, -w[0]};  // cross((0,1,0), w)
+    const double lu = std::sqrt(u[0] * u[0] + u[2] * u[2]);
+    for (double& x : u) x /= lu;
+    const double v[3] = {w[1] * u[2] - w[2] * u[1], w[2] * u[0] - w[0] * u[2], w[0] * u[1] - w[1] * u[0]};
+    for (int a = 0; a < 3; a++) {
+        c.center[a] = f[a];
+        c.du[a] = 0.01 * u[a];
+        c.dv[a] = -0.01 * v[a];
+        c.pixel0[a] = f[a] - 10 * w[a] - 0.8 * u[a] + 0.45 * v[a];
+    }
+    c.t_min = 1e-3; c.t_max = INFINITY;
+    return c;
+}
+
+static void run(const std::vector<rt_sphere>& s, const char* name, bool trained = false) {
+    const double ext = std::fmax(rtbvh::scene_extent(s.data(), s.size()), 25.0);
+    std::vector<rtbvh::TrainRay> rays;
+    if (trained) {
+        const rtbvh::Bvh sah = rtbvh::build(s.data(), s.size(), ext);
+        rays = rtbvh::sample_rays(s.data(), s.size(), look_at(13, 2, 3), sah, 3000, 1);
+        CHECK(rays.size() >= 3000, "%s: %zu training rays", name, rays.size());
+    }
+    const rtbvh::Bvh b = rtbvh::build(s.data(), s.size(), ext, trained ? &rays : nullptr);
     CHECK(b.ok, "%s: build failed", name);
     if (!b.ok) return;
     std::vector<uint32_t> seen;
@@ -72,6 +99,21 @@ static void run(const std::vector<rt_sphere>& s, const char* name) {
         if (k != rtbvh::kSentinel) count.at(k)++;
     for (size_t k = 0; k < s.size(); k++) CHECK(count[k] == 1, "%s: sphere %zu appears %d times", name, k, count[k]);
     check_boxes(b, s, 0);
+    // the host traversal (training-ray sampler) finds the linear scan's closest sphere
+    std::mt19937_64 rng(11);
+    std::normal_distribution<double> N(0, 4);
+    for (int q = 0; q < 2000; q++) {
+        const double o[3] = {N(rng), N(rng), N(rng)}, d[3] = {N(rng), N(rng), N(rng)};
+        double t_tree, t_lin = INFINITY;
+        const int k_tree = rtbvh::closest_hit(b, s.data(), o, d, 1e-3, &t_tree);
+        int k_lin = -1;
+        rtbvh::Bvh flat;  // always-list only: a linear scan through the same arithmetic
+        flat.ok = true;
+        for (uint32_t k = 0; k < s.size(); k++) flat.slot_to_sphere.push_back(k);
+        flat.n_always = (uint32_t)s.size();
+        k_lin = rtbvh::closest_hit(flat, s.data(), o, d, 1e-3, &t_lin);
+        CHECK(k_tree == k_lin && (k_tree < 0 || t_tree == t_lin), "%s: ray %d tree %d lin %d", name, q, k_tree, k_lin);
+    }
     std::printf("%s: n=%zu nodes=%zu slots=%zu always=%u depth=%d\n", name, s.size(), b.nodes.size(),
                 b.slot_to_sphere.size(), b.n_always, maxd);
 }
@@ -97,6 +139,15 @@ int main() {
         s.push_back(sph(0, -1000, 0, 1000));
         s.push_back(sph(INFINITY, 0, 0, 1));
         run(s, "soup");
+        s.pop_back();  // the sampler needs finite geometry to trace; the tree still takes any
+        run(s, "soup_trained", true);
+    }
+    {  // a final-scene-like field: small spheres on a ground sphere, a ray-driven (trained) tree
+        std::vector<rt_sphere> s{sph(0, -1000, 0, 1000)};
+        for (int a = -11; a < 11; a++)
+            for (int c = -11; c < 11; c++) s.push_back(sph(a + 0.9 * U(rng), 0.2, c + 0.9 * U(rng), 0.2));
+        s.push_back(sph(0, 1, 0, 1));
+        run(s, "field_trained", true);
     }
     {  // large scene (15000 full leaves): depth bound must hold (median splits take over)
         std::vector<rt_sphere> s;

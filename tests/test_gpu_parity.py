@@ -266,6 +266,44 @@ def test_bvh_random_scenes_bit_exact(oracle, seed, always_area, monkeypatch):
     assert np.array_equal(out, ref) and st["rays"] == rays
 
 
+@pytest.mark.parametrize("seed", [4, 23, 61])
+def test_trained_tree_random_scenes_bit_exact(oracle, seed, monkeypatch):
+    """Ray-driven trees (RTZIG_BVH_TRAIN=1 forces training on these small launches): the tree built
+    from the camera's sample rays must return the linear scan's bits on random soups."""
+    monkeypatch.setenv("RTZIG_KERNEL", "bvh")
+    monkeypatch.setenv("RTZIG_BVH_TRAIN", "1")
+    rng = np.random.default_rng(1000 + seed)
+    n = int(rng.integers(40, 300))
+    arr = (RtSphere * (n + 1))()
+    for k in range(n):
+        arr[k] = RtSphere(center=D3(*rng.normal(0, 3, 3)), radius=float(rng.choice([rng.uniform(-0.1, 0.01),
+                          rng.uniform(0.01, 0.5), rng.uniform(0.5, 3)])),
+                          material=int(rng.integers(0, 3)), albedo=D3(*rng.uniform(0, 1, 3)),
+                          fuzz=float(rng.uniform(0, 1.2)), refraction_index=float(rng.uniform(0.5, 2.5)))
+    arr[n] = RtSphere(center=D3(0, -1000.5, 0), radius=1000.0, material=0, albedo=D3(0.5, 0.5, 0.5))
+    scene = rtzig.Scene.init(seed)
+    scene.world = arr
+    cam = (rtzig.Camera.builder(96, 1.5).setScene(scene).setDefocusAngle(float(rng.uniform(0, 3)))
+           .setFocusDist(float(rng.uniform(1, 10))).setViewport(tuple(rng.normal(0, 8, 3)), (0, 0, 0),
+                                                               float(rng.uniform(20, 90)))
+           .setSamplesPerPixel(4).build())
+    out, st = gpu_render(cam, arr, n_gpus=1)
+    ref, rays = oracle.render_b(cam.cam, arr, threads=8)
+    assert np.array_equal(out, ref) and st["rays"] == rays
+
+
+@pytest.mark.parametrize("mode", ["ring", "direct"])
+def test_trained_tree_final_scene_bit_exact(oracle, mode, monkeypatch):
+    """The bench's scene and camera with the tree trained on its rays (what config 4 runs), on a
+    reduced image: every pixel bit-exact, in both unit modes."""
+    monkeypatch.setenv("RTZIG_BVH_TRAIN", "1")
+    monkeypatch.setenv("RTZIG_UNIT_MODE", mode)
+    cam = rtzig.final_scene_camera(width=240, aspect_ratio=1.5, spp=6)
+    out, st = gpu_render(cam, cam.scene.world, n_gpus=1)
+    ref, rays = oracle.render_b(cam.cam, cam.scene.world, threads=8)
+    assert np.array_equal(out, ref) and st["rays"] == rays
+
+
 def test_bvh_far_camera_rebuild(oracle, monkeypatch):
     """A camera far outside the scene's extent raises the BVH padding's origin bound (rebuild)."""
     monkeypatch.setenv("RTZIG_KERNEL", "bvh")

@@ -1,0 +1,266 @@
+// bvh_sim.cpp — CPU model of the BVH walk's cost for tree-build experiments (no GPU).
+//
+// Traces a sample of the final scene's paths (the reference's camera and scatter rules, any RNG:
+// only the ray distribution matters here), records every ray segment, then replays the kernel's
+// walk (always-list first, near-child-first traversal of the f32 boxes against [t_min, closest],
+// kLeafMax-slot leaves) over the tree rtbvh::build produces, and reports
+//   visits/ray   internal-node visits per ray (the kernel's instrumented `node_visits_per_ray`)
+//   leaves/ray   leaf rounds per ray
+//   wave steps   while-while inner steps per 64-ray wave: sum over segments k of the max over the
+//                wave's lanes of the inner steps before the lane's k-th leaf (rays shuffled into
+//                waves, as the persistent kernel mixes paths)
+//
+//   g++ -O2 -std=c++17 tools/bvh_sim.cpp raytracing-with-zig_amd/csrc/rt_bvh.cpp \
+//       raytracing-with-zig_amd/csrc/rt_host.cpp -o /tmp/bvh_sim && /tmp/bvh_sim [stride] [spp] [train_stride (<0: surface rays)] [n_samples: rtbvh::sample_rays]
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <random>
+#include <vector>
+
+#include "../include/rt.h"
+#include "../raytracing-with-zig_amd/csrc/rt_bvh.hpp"
+
+// rt_host.cpp's Camera::render calls the GPU entry point; the simulator never does
+extern "C" int rt_render(const rt_camera*, const rt_sphere*, size_t, const rt_options*, void*) { return -1; }
+
+struct V {
+    double x, y, z;
+};
+static V operator+(V a, V b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }
+static V operator-(V a, V b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
+static V operator*(V a, double s) { return {a.x * s, a.y * s, a.z * s}; }
+static double dot(V a, V b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+static V unit(V a) { return a * (1.0 / std::sqrt(dot(a, a))); }
+static V mkv(const double* p) { return {p[0], p[1], p[2]}; }
+
+static double hit_sphere(const rt_sphere& s, V o, V d, double tmin, double closest) {
+    const V oc = mkv(s.center) - o;
+    const double a = dot(d, d), h = dot(d, oc), c = dot(oc, oc) - s.radius * s.radius;
+    const double disc = h * h - a * c;
+    if (disc < 0) return INFINITY;
+    const double sq = std::sqrt(disc);
+    double r = (h - sq) / a;
+    if (!(tmin < r && r < closest)) {
+        r = (h + sq) / a;
+        if (!(tmin < r && r < closest)) return INFINITY;
+    }
+    return r;
+}
+
+struct Ray {
+    V o, d;
+    double t;  // closest hit (+inf: miss)
+};
+
+int main(int argc, char** argv) {
+    const int stride = argc > 1 ? std::atoi(argv[1]) : 4;
+    const int spp = argc > 2 ? std::atoi(argv[2]) : 1;
+    std::vector<rt_sphere> sp(600);
+    size_t n = 0;
+    rt_scene_final(0xDEADBEEF, sp.data(), sp.size(), &n, nullptr);
+    sp.resize(n);
+    for (auto& s : sp) s.radius = s.radius > 0 ? s.radius : 0;
+    rt_camera_params p{};
+    p.image_width = 1200; p.samples_per_pixel = spp; p.bounce_max = 50; p.aspect_ratio = 1.5;
+    p.look_from[0] = 13; p.look_from[1] = 2; p.look_from[2] = 3;
+    p.v_up[1] = 1; p.vfov = 20; p.defocus_angle = 0.6; p.focus_dist = 10; p.t_min = 1e-3; p.t_max = INFINITY;
+    rt_camera cam;
+    rt_camera_build(&p, &cam);
+
+    // ---- trace a sample of paths, record every ray segment ----
+    std::mt19937_64 rng(12345);
+    auto trace = [&](uint64_t seed, int stride, int spp, std::vector<Ray>& rays) {
+    rng.seed(seed);
+    std::uniform_real_distribution<double> U(0.0, 1.0);
+    auto ruv = [&]() {
+        while (true) {
+            V q{2 * U(rng) - 1, 2 * U(rng) - 1, 2 * U(rng) - 1};
+            const double l = dot(q, q);
+            if (1e-160 < l && l <= 1) return q * (1.0 / std::sqrt(l));
+        }
+    };
+    for (uint32_t j = 0; j < cam.image_height; j += stride)
+        for (uint32_t i = 0; i < cam.image_width; i += stride)
+            for (int s = 0; s < spp; s++) {
+                const V ps = mkv(cam.pixel0) + mkv(cam.du) * (i + U(rng) - 0.5) + mkv(cam.dv) * (j + U(rng) - 0.5);
+                double px, py;
+                do { px = 2 * U(rng) - 1; py = 2 * U(rng) - 1; } while (px * px + py * py >= 1);
+                V o = mkv(cam.center) + mkv(cam.defocus_disk_u) * px + mkv(cam.defocus_disk_v) * py;
+                V d = ps - o;
+                for (uint32_t b = 0; b < cam.bounce_max; b++) {
+                    double best = INFINITY;
+                    int k = -1;
+                    for (size_t q = 0; q < n; q++) {
+                        const double t = hit_sphere(sp[q], o, d, 1e-3, best);
+                        if (t < best) { best = t; k = (int)q; }
+                    }
+                    rays.push_back({o, d, best});
+                    if (k < 0) break;
+                    const rt_sphere& S = sp[k];
+                    const V pt = o + d * best;
+                    const V out = (pt - mkv(S.center)) * (1.0 / S.radius);
+                    const bool front = dot(d, out) < 0;
+                    const V nrm = front ? out : out * -1.0;
+                    if (S.material == RT_LAMBERTIAN) {
+                        V nd = nrm + ruv();
+                        if (std::fabs(nd.x) < 1e-8 && std::fabs(nd.y) < 1e-8 && std::fabs(nd.z) < 1e-8) nd = nrm;
+                        d = nd;
+                    } else if (S.material == RT_METAL) {
+                        const V r = unit(d - nrm * (2 * dot(d, nrm)));
+                        d = r + ruv() * S.fuzz;
+                        if (!(dot(d, nrm) > 0)) break;
+                    } else {
+                        const double ri = front ? 1.0 / S.refraction_index : S.refraction_index;
+                        const V u = unit(d);
+                        const double ct = std::fmin(dot(u * -1.0, nrm), 1.0), st = std::sqrt(1 - ct * ct);
+                        double r0 = (1 - ri) / (1 + ri); r0 *= r0;
+                        const double sch = r0 + (1 - r0) * std::pow(1 - ct, 5);
+                        if (ri * st > 1 || sch > U(rng)) {
+                            d = u - nrm * (2 * dot(u, nrm));
+                        } else {
+                            const V perp = (u + nrm * ct) * ri;
+                            const V par = nrm * -std::sqrt(std::fabs(1 - dot(perp, perp)));
+                            d = perp + par;
+                        }
+                    }
+                    o = pt;
+                }
+            }
+    std::shuffle(rays.begin(), rays.end(), rng);
+    };
+    std::vector<Ray> rays, train_rays;
+    trace(12345, stride, spp, rays);
+    std::fprintf(stderr, "%zu test rays\n", rays.size());
+    const int tstride = argc > 3 ? std::atoi(argv[3]) : 0;  // 0: plain SAH build
+    std::vector<rtbvh::TrainRay> train;
+    if (tstride < 0) {
+        // camera-independent training set: diffuse rays leaving random surface points of the
+        // boundable spheres (uniform over spheres and over each sphere's surface) and of the ground
+        // within the other spheres' xz extent
+        rng.seed(777);
+        std::uniform_real_distribution<double> U(0.0, 1.0);
+        const size_t want = (size_t)(-tstride) * 1000;
+        double xlo = 1e300, xhi = -1e300, zlo = 1e300, zhi = -1e300;
+        for (auto& s : sp) if (s.radius < 100) {
+            xlo = std::min(xlo, s.center[0] - s.radius); xhi = std::max(xhi, s.center[0] + s.radius);
+            zlo = std::min(zlo, s.center[2] - s.radius); zhi = std::max(zhi, s.center[2] + s.radius);
+        }
+        while (train_rays.size() < want) {
+            const size_t k = (size_t)(U(rng) * n);
+            const rt_sphere& S = sp[k];
+            V nrm, o;
+            if (S.radius >= 100) {
+                const double x = xlo + U(rng) * (xhi - xlo), z = zlo + U(rng) * (zhi - zlo);
+                const V c = mkv(S.center);
+                nrm = unit(V{x, 0, z} - c);
+                o = c + nrm * S.radius;
+            } else {
+                V q;
+                do { q = {2 * U(rng) - 1, 2 * U(rng) - 1, 2 * U(rng) - 1}; } while (dot(q, q) > 1 || dot(q, q) < 1e-6);
+                nrm = unit(q);
+                o = mkv(S.center) + nrm * S.radius;
+            }
+            V q;
+            do { q = {2 * U(rng) - 1, 2 * U(rng) - 1, 2 * U(rng) - 1}; } while (dot(q, q) > 1 || dot(q, q) < 1e-6);
+            const V d = nrm + unit(q);
+            double best = INFINITY;
+            for (size_t j = 0; j < n; j++) best = std::min(best, hit_sphere(sp[j], o, d, 1e-3, best));
+            train_rays.push_back({o, d, best});
+        }
+        for (const Ray& r : train_rays) train.push_back({{r.o.x, r.o.y, r.o.z}, {r.d.x, r.d.y, r.d.z}, r.t});
+    }
+    if (tstride > 0 && argc > 4) {  // the library's own sampler (rtbvh::sample_rays) over the SAH tree
+        const double ob0 = std::max(rtbvh::scene_extent(sp.data(), n), 13.5);
+        const rtbvh::Bvh sah = rtbvh::build(sp.data(), n, ob0);
+        train = rtbvh::sample_rays(sp.data(), n, cam, sah, (size_t)std::atoi(argv[4]), 0x5eed);
+        std::fprintf(stderr, "%zu training rays (sample_rays)\n", train.size());
+    } else if (tstride > 0) {
+        trace(777, tstride, 1, train_rays);
+        for (const Ray& r : train_rays) train.push_back({{r.o.x, r.o.y, r.o.z}, {r.d.x, r.d.y, r.d.z}, r.t});
+        std::fprintf(stderr, "%zu training rays\n", train.size());
+    }
+
+    // ---- replay the walk over the built tree ----
+    const double ob = std::max(rtbvh::scene_extent(sp.data(), n), 13.5);
+    rtbvh::Bvh bvh = rtbvh::build(sp.data(), n, ob, tstride != 0 ? &train : nullptr);
+    if (!bvh.ok) { std::fprintf(stderr, "build failed\n"); return 1; }
+    const size_t na = bvh.n_always;
+    double visits = 0, leaves = 0, wave_steps = 0, wave_leaf = 0, tests = 0;
+    std::vector<std::vector<int>> runs(64);
+    size_t nw = 0;
+    for (size_t w0 = 0; w0 + 64 <= rays.size(); w0 += 64, ++nw) {
+        size_t maxleaf = 0;
+        for (int l = 0; l < 64; l++) {
+            const Ray& R = rays[w0 + l];
+            runs[l].clear();
+            double closest = INFINITY;
+            for (size_t q = 0; q < na; q++) closest = std::min(closest, hit_sphere(sp[bvh.slot_to_sphere[q]], R.o, R.d, 1e-3, closest));
+            const float inv[3] = {1.0f / (float)R.d.x, 1.0f / (float)R.d.y, 1.0f / (float)R.d.z};
+            const float org[3] = {(float)R.o.x, (float)R.o.y, (float)R.o.z};
+            auto box = [&](const float* lo, const float* hi, float& tn) {
+                float t0 = 1e-3f, t1 = (float)closest * (1 + 1e-6f);
+                for (int a = 0; a < 3; a++) {
+                    float ta = (lo[a] - org[a]) * inv[a], tb = (hi[a] - org[a]) * inv[a];
+                    if (ta > tb) std::swap(ta, tb);
+                    t0 = std::max(t0, ta);
+                    t1 = std::min(t1, tb);
+                }
+                tn = t0;
+                return t0 <= t1;
+            };
+            std::vector<int32_t> stack;
+            int32_t cur = 0;
+            int run = 0;
+            while (true) {
+                if (cur >= 0) {
+                    const rtbvh::Node& nd = bvh.nodes[cur];
+                    ++run;
+                    visits++;
+                    float n0, n1;
+                    const bool h0 = box(nd.lo0, nd.hi0, n0), h1 = box(nd.lo1, nd.hi1, n1);
+                    if (h0 && h1) {
+                        const bool f0 = n0 <= n1;
+                        stack.push_back(f0 ? nd.ref1 : nd.ref0);
+                        cur = f0 ? nd.ref0 : nd.ref1;
+                    } else if (h0 || h1) {
+                        cur = h0 ? nd.ref0 : nd.ref1;
+                    } else {
+                        if (stack.empty()) break;
+                        cur = stack.back();
+                        stack.pop_back();
+                    }
+                } else {
+                    runs[l].push_back(run);
+                    run = 0;
+                    leaves++;
+                    const size_t base = na + (size_t)rtbvh::kLeafMax * (size_t)(~cur);
+                    for (int u = 0; u < rtbvh::kLeafMax; u++) {
+                        const uint32_t k = bvh.slot_to_sphere[base + u];
+                        if (k == rtbvh::kSentinel) continue;
+                        tests++;
+                        closest = std::min(closest, hit_sphere(sp[k], R.o, R.d, 1e-3, closest));
+                    }
+                    if (stack.empty()) break;
+                    cur = stack.back();
+                    stack.pop_back();
+                }
+            }
+            runs[l].push_back(run);
+            maxleaf = std::max(maxleaf, runs[l].size() - 1);
+        }
+        wave_leaf += (double)maxleaf;
+        for (size_t k = 0; k <= maxleaf; k++) {
+            int m = 0;
+            for (int l = 0; l < 64; l++)
+                if (k < runs[l].size()) m = std::max(m, runs[l][k]);
+            wave_steps += m;
+        }
+    }
+    const double nr = (double)nw * 64;
+    std::printf("{\"nodes\": %zu, \"depth\": %d, \"n_always\": %zu, \"visits_per_ray\": %.4f, \"leaves_per_ray\": %.4f, "
+                "\"leaf_tests_per_ray\": %.4f, \"wave_inner_steps\": %.3f, \"wave_leaf_rounds\": %.3f}\n",
+                bvh.nodes.size(), bvh.depth, na, visits / nr, leaves / nr, tests / nr, wave_steps / nw, wave_leaf / nw);
+    return 0;
+}
