@@ -27,7 +27,10 @@ constexpr double kAlwaysRel = 10.0;   // ... or box area above this multiple of 
 constexpr int kMaxBig = 4;           // at most this many such spheres
 constexpr uint32_t kSentinel = 0xffffffffu;  // slot_to_sphere value of a padding slot
 constexpr size_t kMinTrain = 64;             // ray-driven splits need at least this many segments
-constexpr double kRayCostExp = 0.4;          // ray-driven split cost: segments x spheres^kRayCostExp
+#ifndef RTZIG_RAYCOST_EXP
+#define RTZIG_RAYCOST_EXP 0.4
+#endif
+constexpr double kRayCostExp = RTZIG_RAYCOST_EXP;  // ray-driven split cost: segments x spheres^kRayCostExp (build knob)
 
 // Internal node: the boxes of both children (f32, padded outward) and their refs.
 // ref >= 0: internal node index; ref < 0: leaf index ~ref.  Leaf L holds slots

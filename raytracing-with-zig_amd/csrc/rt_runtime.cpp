@@ -62,7 +62,10 @@ struct SceneData {
 // kTrainSamples camera samples.  Config 4: node visits per ray 6.97 -> 6.2.
 constexpr uint64_t kTrainMinSamples = 1ull << 25;
 constexpr size_t kTrainMinSpheres = 32;
-constexpr size_t kTrainSamples = 6000;
+#ifndef RTZIG_TRAIN_SAMPLES
+#define RTZIG_TRAIN_SAMPLES 6000
+#endif
+constexpr size_t kTrainSamples = RTZIG_TRAIN_SAMPLES;  // build knob
 constexpr uint64_t kTrainSeed = 0x7261792d74726565ull;
 constexpr size_t kLdsTreeBytes = 80 * 1024;  // rtk_launch_samples_bvh's LDS budget per block
 
