@@ -81,17 +81,39 @@ struct Builder {
         return ~(int32_t)index;
     }
 
-    // does the sample segment [t_min, tmax] of ray `r` enter the box?  (f64 slabs; a zero direction
-    // component tests the origin against that slab)
-    static bool seg_hits(const TrainRay& r, const double lo[3], const double hi[3]) {
+    // a sample segment with its inverse direction (zero components flagged: those slabs test the
+    // origin instead)
+    struct Seg {
+        double o[3], inv[3], tmax;
+        unsigned zero;  // bit a: d[a] == 0
+    };
+    std::vector<Seg> segs;
+    void set_train(const std::vector<TrainRay>* t) {
+        train = t;
+        if (!t) return;
+        segs.resize(t->size());
+        for (size_t i = 0; i < t->size(); i++) {
+            const TrainRay& r = (*t)[i];
+            Seg& g = segs[i];
+            g.zero = 0;
+            g.tmax = r.tmax;
+            for (int a = 0; a < 3; a++) {
+                g.o[a] = r.o[a];
+                g.inv[a] = r.d[a] == 0 ? 0.0 : 1.0 / r.d[a];
+                if (r.d[a] == 0) g.zero |= 1u << a;
+            }
+        }
+    }
+
+    // does the sample segment [t_min, tmax] enter the box?  (f64 slabs)
+    static bool seg_hits(const Seg& r, const double lo[3], const double hi[3]) {
         double t0 = 1e-3, t1 = r.tmax;
         for (int a = 0; a < 3; a++) {
-            if (r.d[a] == 0) {
+            if (r.zero >> a & 1u) {
                 if (r.o[a] < lo[a] || r.o[a] > hi[a]) return false;
                 continue;
             }
-            const double inv = 1.0 / r.d[a];
-            double ta = (lo[a] - r.o[a]) * inv, tb = (hi[a] - r.o[a]) * inv;
+            double ta = (lo[a] - r.o[a]) * r.inv[a], tb = (hi[a] - r.o[a]) * r.inv[a];
             if (ta > tb) std::swap(ta, tb);
             t0 = std::max(t0, ta);
             t1 = std::min(t1, tb);
@@ -127,7 +149,7 @@ struct Builder {
         }
         std::vector<double> first_l(n + 1, 0.0), last_r(n + 1, 0.0);  // histograms
         for (uint32_t ri : rays) {
-            const TrainRay& r = (*train)[ri];
+            const Seg& r = segs[ri];
             if (seg_hits(r, &L[6 * (n - 1)], &L[6 * (n - 1) + 3])) {
                 size_t l = 1, h = n - 1;  // smallest i with a hit
                 while (l < h) {
@@ -232,10 +254,10 @@ struct Builder {
             double lo[3], hi[3];
             bounds(b, best_split, lo, hi);
             for (uint32_t ri : rays)
-                if (seg_hits((*train)[ri], lo, hi)) rays0.push_back(ri);
+                if (seg_hits(segs[ri], lo, hi)) rays0.push_back(ri);
             bounds(best_split, e, lo, hi);
             for (uint32_t ri : rays)
-                if (seg_hits((*train)[ri], lo, hi)) rays1.push_back(ri);
+                if (seg_hits(segs[ri], lo, hi)) rays1.push_back(ri);
         }
         const int32_t r0 = build(b, best_split, depth + 1, rays0);
         const int32_t r1 = build(best_split, e, depth + 1, rays1);
@@ -275,7 +297,7 @@ Bvh build(const rt_sphere* spheres, size_t n, double origin_bound, const std::ve
     Bvh out;
     out.origin_bound = origin_bound;
     Builder B;
-    B.train = train;
+    B.set_train(train);
     std::vector<uint32_t> always;
     const double e_origin = std::ldexp(origin_bound, -21);
     for (size_t k = 0; k < n; k++) {
@@ -355,7 +377,7 @@ Bvh build(const rt_sphere* spheres, size_t n, double origin_bound, const std::ve
             double lo[3], hi[3];
             B.bounds(0, m, lo, hi);
             for (size_t i = 0; i < train->size(); i++)
-                if (Builder::seg_hits((*train)[i], lo, hi)) rays.push_back((uint32_t)i);
+                if (Builder::seg_hits(B.segs[i], lo, hi)) rays.push_back((uint32_t)i);
         }
         B.build(0, m, 1, rays);
     }

@@ -13,6 +13,7 @@
 //   g++ -O2 -std=c++17 tools/bvh_sim.cpp raytracing-with-zig_amd/csrc/rt_bvh.cpp \
 //       raytracing-with-zig_amd/csrc/rt_host.cpp -o /tmp/bvh_sim && /tmp/bvh_sim [stride] [spp] [train_stride (<0: surface rays)] [n_samples: rtbvh::sample_rays]
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -172,10 +173,14 @@ int main(int argc, char** argv) {
         for (const Ray& r : train_rays) train.push_back({{r.o.x, r.o.y, r.o.z}, {r.d.x, r.d.y, r.d.z}, r.t});
     }
     if (tstride > 0 && argc > 4) {  // the library's own sampler (rtbvh::sample_rays) over the SAH tree
+        const auto t0 = std::chrono::steady_clock::now();
         const double ob0 = std::max(rtbvh::scene_extent(sp.data(), n), 13.5);
         const rtbvh::Bvh sah = rtbvh::build(sp.data(), n, ob0);
         train = rtbvh::sample_rays(sp.data(), n, cam, sah, (size_t)std::atoi(argv[4]), 0x5eed);
-        std::fprintf(stderr, "%zu training rays (sample_rays)\n", train.size());
+        const rtbvh::Bvh trained = rtbvh::build(sp.data(), n, ob0, &train);
+        const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        std::fprintf(stderr, "%zu training rays (sample_rays); SAH build + sampling + trained build %.1f ms\n",
+                     train.size(), ms);
     } else if (tstride > 0) {
         trace(777, tstride, 1, train_rays);
         for (const Ray& r : train_rays) train.push_back({{r.o.x, r.o.y, r.o.z}, {r.d.x, r.d.y, r.d.z}, r.t});
