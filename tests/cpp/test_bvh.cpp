@@ -149,6 +149,14 @@ int main() {
         s.push_back(sph(0, 1, 0, 1));
         run(s, "field_trained", true);
     }
+    {  // degenerate training input: zero and negative radii, coincident spheres (NaN normals in the
+       // sampler's scatter) must still give a valid tree
+        std::vector<rt_sphere> s;
+        for (int k = 0; k < 200; k++) s.push_back(sph(N(rng) * 0.3, N(rng) * 0.3, N(rng) * 0.3, k % 3 ? 0.0 : -1.0));
+        for (int k = 0; k < 100; k++) s.push_back(sph(0.5, 0.5, 0.5, 0.3));
+        s.push_back(sph(0, -1000, 0, 1000));
+        run(s, "degenerate_trained", true);
+    }
     {  // large scene (15000 full leaves): depth bound must hold (median splits take over)
         std::vector<rt_sphere> s;
         for (int k = 0; k < 15000 * rtbvh::kLeafMax; k++) s.push_back(sph(N(rng) * 10, N(rng), N(rng) * 10, 0.1));
