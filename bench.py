@@ -179,8 +179,15 @@ def main():
             img = rdist.gather_image(out, H, rank, world)
         return img
 
-    for _ in range(args.warmup):
+    # the first frame also pays the one-time BVH rebuild from sample rays of this camera (DESIGN.md
+    # §5 "Ray-driven tree"): its wall time is reported as a fixed cost
+    first_ms = None
+    for w in range(args.warmup):
+        t_w = time.perf_counter()
         frame()
+        torch.cuda.synchronize()
+        if w == 0:
+            first_ms = (time.perf_counter() - t_w) * 1e3
     # one untimed instrumented frame: exact executed-work counts (sphere tests, BVH node visits)
     pstats = torch.zeros(24, dtype=torch.int64, device=dev)
     if n_rows:
@@ -331,7 +338,8 @@ def main():
                              f"the reduce pass, {n_rows * W * spp * 48 / 1e9:.2f} GB per frame"),
             },
             "rays_per_sample": round(rays_per_frame / max(1, samples_per_frame), 4),
-            "fixed_costs_ms": {"context_and_scene_upload": round(init_ms, 2)},
+            "fixed_costs_ms": {"context_and_scene_upload": round(init_ms, 2),
+                               "first_frame_incl_bvh_training": round(first_ms, 2) if first_ms else None},
             "cpu_baseline": None,
             "fast_f32": fast,
         }
