@@ -187,6 +187,25 @@ int main(int argc, char** argv) {
         std::fprintf(stderr, "%zu training rays\n", train.size());
     }
 
+    // optional: regroup each batch of `group` consecutive rays by a coherence key before forming
+    // 64-ray waves (upper bound of what regrouping rays across a block's waves could give)
+    if (const char* e = std::getenv("SIM_GROUP")) {
+        const size_t group = (size_t)std::atoi(e);
+        const int key_mode = std::getenv("SIM_KEY") ? std::atoi(std::getenv("SIM_KEY")) : 0;
+        auto key = [&](const Ray& r) -> uint64_t {
+            const uint64_t oct = (r.d.x < 0) | (r.d.y < 0) << 1 | (r.d.z < 0) << 2;
+            if (key_mode == 0) return oct;
+            // octant + coarse origin cell (2-unit cells over [-16, 16)^3)
+            auto cell = [](double v) { return (uint64_t)std::min(15.0, std::max(0.0, (v + 16) / 2)); };
+            const uint64_t c = cell(r.o.x) | cell(r.o.y) << 4 | cell(r.o.z) << 8;
+            if (key_mode == 1) return oct << 12 | c;
+            return c << 3 | oct;
+        };
+        for (size_t b = 0; b + group <= rays.size(); b += group)
+            std::stable_sort(rays.begin() + b, rays.begin() + b + group,
+                             [&](const Ray& x, const Ray& y) { return key(x) < key(y); });
+    }
+
     // ---- replay the walk over the built tree ----
     const double ob = std::max(rtbvh::scene_extent(sp.data(), n), 13.5);
     rtbvh::Bvh bvh = rtbvh::build(sp.data(), n, ob, tstride != 0 ? &train : nullptr);
