@@ -161,7 +161,8 @@ int rt_context_kernel_times_total(rt_context* ctx, double* sample_ms, double* re
  * root division), wave-level second-root divisions, node visits of camera rays, sphere tests of
  * camera rays, [13..15] kernel timeline stamps, [16] wave-cycles in the rejection-trip loop,
  * [17] idle sleeps of waves waiting on a hand-off, [18] deferred unit finalisations (previous chunk
- * of the tile not yet finalised), [19] refills that found no free ring slot, 0...}.  Counts 0-3 are
+ * of the tile not yet finalised), [19] refills that found no free ring slot, [20] / [21] sum / max over
+ * waves of (wave end - the wave's first empty claim), [22] the last wave's first empty claim, 0}.  Counts 0-3 are
  * exact and deterministic; the cycles and wave-iteration counts are diagnostics. */
 int rt_context_enable_profile(rt_context* ctx, int enable);
 

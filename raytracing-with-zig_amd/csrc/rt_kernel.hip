@@ -878,6 +878,11 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
                 atomicMax(&stats[13], (unsigned long long)~rt_start);
                 atomicMax(&stats[14], (unsigned long long)~rt_drain);
                 atomicMax(&stats[15], (unsigned long long)rt_end);
+                // drain-tail shape: sum and max over waves of (own end - own drain), last drain
+                const uint64_t own_tail = rt_drain ? rt_end - rt_drain : 0;
+                atomicAdd(&stats[20], (unsigned long long)own_tail);
+                atomicMax(&stats[21], (unsigned long long)own_tail);
+                atomicMax(&stats[22], (unsigned long long)rt_drain);
             }
             uint64_t wi = pr.w_inner, wl = pr.w_leaf, wc = pr.w_cand, w2 = pr.w_root2;
             for (int off = 32; off > 0; off >>= 1) {

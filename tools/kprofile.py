@@ -15,6 +15,7 @@ import torch  # noqa: E402
 
 import rtzig  # noqa: E402
 
+res_waves = torch.cuda.get_device_properties(0).multi_processor_count * 16 if torch.cuda.is_available() else 4096  # persistent grid: 16 waves per CU
 ap = argparse.ArgumentParser()
 ap.add_argument("--width", type=int, default=1200)
 ap.add_argument("--aspect", type=float, default=1.5)
@@ -70,7 +71,11 @@ for v in args.variants.split():
         "timeline_us": {"first_wave_start_to_first_drain": round(((~s[14] & (2**64 - 1)) - (~s[13] & (2**64 - 1))) / 100, 1)
                         if s[14] else None,
                         "first_drain_to_last_wave_end": round((s[15] - (~s[14] & (2**64 - 1))) / 100, 1)
-                        if s[14] else None},
+                        if s[14] else None,
+                        "first_drain_to_last_drain": round((s[22] - (~s[14] & (2**64 - 1))) / 100, 1)
+                        if s[14] and s[22] else None,
+                        "wave_tail_avg (own drain to own end)": round(s[20] / 100 / max(1, res_waves), 1),
+                        "wave_tail_max": round(s[21] / 100, 1)},
         "cycle_split": {"refill": round(s[4] / cyc, 4), "walk": round(s[5] / cyc, 4), "shade": round(s[6] / cyc, 4), "trips": round(s[16] / cyc, 4)},
         "scheduler": {"idle_sleeps": s[17], "deferred_finalisations": s[18], "refills_without_free_slot": s[19]},
         "raw": s,
