@@ -1066,9 +1066,11 @@ struct Variant {
 };
 constexpr Variant kVariants[] = {{"lds_u4", true, 4, 1}, {"smem_u4", false, 4, 1}};
 
-const Variant& variant_choice(bool fits_lds) {
+const Variant& variant_choice(bool fits_lds, uint32_t n_pad) {
     const char* e = std::getenv("RTZIG_KERNEL");
-    const char* want = e ? e : rtk::kDefaultVariant;
+    // tiny scenes (the runtime's list-walk case, rt_runtime.cpp use_bvh): LDS broadcasts beat scalar
+    // loads there (chapter 13: 9.50 against 9.80 ms at 100 spp)
+    const char* want = e ? e : (n_pad <= 8 ? "lds_u4" : rtk::kDefaultVariant);
     for (const Variant& v : kVariants)
         if (std::strcmp(v.name, want) == 0 && (fits_lds || !v.lds)) return v;
     for (const Variant& v : kVariants)
@@ -1084,7 +1086,7 @@ extern "C" hipError_t rtk_launch_samples(const rtk::KernelParams* p, const rtk::
     using namespace rtk;
     const uint64_t total = (uint64_t)p->n_rows * p->width * p->s_count;
     if (total == 0) return hipSuccess;
-    const Variant& v = variant_choice(p->n_pad <= kMaxLdsSpheres);
+    const Variant& v = variant_choice(p->n_pad <= kMaxLdsSpheres, p->n_pad);
     const size_t shmem = v.lds ? (size_t)p->n_pad * sizeof(GeoRec) : 0;
     const uint64_t need = (total + kBlock - 1) / kBlock;
     auto* st = (unsigned long long*)stats;

@@ -68,6 +68,7 @@ constexpr size_t kTrainMinSpheres = 32;
 constexpr size_t kTrainSamples = RTZIG_TRAIN_SAMPLES;  // build knob
 constexpr uint64_t kTrainSeed = 0x7261792d74726565ull;
 constexpr size_t kLdsTreeBytes = 80 * 1024;  // rtk_launch_samples_bvh's LDS budget per block
+constexpr uint32_t kLinearMaxSpheres = 8;    // scenes this small walk the list (use_bvh)
 
 }  // namespace
 
@@ -417,10 +418,13 @@ int upload_scene(rt_context* ctx, const SceneData& sd) {
 }
 
 // Walk selection: RTZIG_KERNEL names a linear variant (lds_u4, smem_u4) or "bvh"; default: the
-// BVH walk when it built, else the linear default variant.
+// BVH walk when it built, except for tiny scenes in f64, where the list walk in LDS is faster
+// (chapter 9's 2 spheres -11.5%, chapter 13's 5 spheres -2%: profiles/r02_walk_ab/).  Fast mode
+// (f32) always walks the tree.
 bool use_bvh(const rt_context* ctx) {
     const char* e = std::getenv("RTZIG_KERNEL");
-    if (e && std::strncmp(e, "bvh", 3) != 0) return false;
+    if (e) return std::strncmp(e, "bvh", 3) == 0 && ctx->scene.bvh_ok;
+    if (ctx->precision == RT_PRECISION_F64 && ctx->n_spheres <= kLinearMaxSpheres) return false;
     return ctx->scene.bvh_ok;
 }
 
