@@ -133,6 +133,7 @@ struct KernelParams {
 // spread over the whole bank row.  Leaves (2 slots: 80 B = 5 x 16, read as ds_read_b128) start
 // at the next 16-B boundary after the nodes.
 constexpr int kBlockBvh = 512;     // 8 waves; 2 blocks per CU share the LDS budget
+constexpr size_t kLdsSceneBudget = 80 * 1024;  // tree + stacks of one block (2 blocks per CU's 160 KiB)
 constexpr int kMaxDepthBvh = 16;   // == rtbvh::kMaxDepth: bound on per-lane LDS stack entries (entry 0: "done")
 #ifndef RTZIG_LEAF
 #define RTZIG_LEAF 2

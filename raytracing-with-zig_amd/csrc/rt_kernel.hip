@@ -1111,7 +1111,7 @@ extern "C" hipError_t rtk_launch_samples_bvh(const rtk::KernelParams* p, const r
     const size_t stack_bytes = (size_t)b->stack_depth * kBlockBvh * sizeof(int32_t);
     const size_t scene_bytes = (size_t)bvh_leaves_offset(b->n_nodes) + (size_t)b->n_leaves * sizeof(BvhLeaf);
     // scene in LDS when two blocks (16 waves) still fit a CU's 160 KiB
-    const bool lds_scene = stack_bytes + scene_bytes <= 80 * 1024;
+    const bool lds_scene = stack_bytes + scene_bytes <= kLdsSceneBudget;
     const size_t shmem = stack_bytes + (lds_scene ? scene_bytes : 0);
     const uint64_t need = (total + kBlockBvh - 1) / kBlockBvh;
     auto* st = (unsigned long long*)stats;

@@ -67,7 +67,6 @@ constexpr size_t kTrainMinSpheres = 32;
 #endif
 constexpr size_t kTrainSamples = RTZIG_TRAIN_SAMPLES;  // build knob
 constexpr uint64_t kTrainSeed = 0x7261792d74726565ull;
-constexpr size_t kLdsTreeBytes = 80 * 1024;  // rtk_launch_samples_bvh's LDS budget per block
 constexpr uint32_t kLinearMaxSpheres = 8;    // scenes this small walk the list (use_bvh)
 
 }  // namespace
@@ -294,7 +293,7 @@ void train_bvh(SceneData& sd, const rt_camera& cam) {
     SceneData sah_sd = sd;
     set_tree(sah_sd, sah, bound);
     set_tree(sd, tree, bound);
-    if (!sd.bvh_ok || (lds_bytes(sd) > kLdsTreeBytes && lds_bytes(sah_sd) <= kLdsTreeBytes)) {
+    if (!sd.bvh_ok || (lds_bytes(sd) > rtk::kLdsSceneBudget && lds_bytes(sah_sd) <= rtk::kLdsSceneBudget)) {
         sd = sah_sd;
         return;
     }
