@@ -520,3 +520,29 @@ def test_device_renderer_alternating_streams_and_cameras(oracle):
     assert np.array_equal(o1.cpu().numpy(), ref1)
     assert np.array_equal(o2.cpu().numpy(), ref2)
     r.close()
+
+
+def test_trained_tree_retrains_per_camera_across_streams(oracle, monkeypatch):
+    """RTZIG_BVH_TRAIN=1: every camera switch rebuilds the tree from that camera's rays and
+    re-uploads it while the previous render (on another stream) may still walk the old one; the
+    context waits for it first (quiesce), so both cameras' images stay exact on every pass."""
+    import torch
+    monkeypatch.setenv("RTZIG_BVH_TRAIN", "1")
+    cam1 = rtzig.final_scene_camera(width=160, aspect_ratio=16 / 9, spp=6)
+    cam2 = (rtzig.Camera.builder(160, 16 / 9).setScene(cam1.scene).setDefocusAngle(0.3).setFocusDist(6)
+            .setViewport((-5, 1.5, 9), (0, 0.3, 0), 30).setSamplesPerPixel(5).build())
+    r = rtzig.DeviceRenderer(0)
+    r.set_scene(cam1.scene.world)
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    o1 = torch.zeros((cam1.height, 160, 3), dtype=torch.float64, device="cuda:0")
+    o2 = torch.zeros((cam2.height, 160, 3), dtype=torch.float64, device="cuda:0")
+    ref1, _ = oracle.render_b(cam1.cam, cam1.scene.world, threads=16)
+    ref2, _ = oracle.render_b(cam2.cam, cam1.scene.world, threads=16)
+    for _ in range(3):
+        r.render_rows_async(cam1.cam, o1.data_ptr(), stream_ptr=s1.cuda_stream)
+        r.render_rows_async(cam2.cam, o2.data_ptr(), stream_ptr=s2.cuda_stream)
+        torch.cuda.synchronize()
+        assert np.array_equal(o1.cpu().numpy(), ref1)
+        assert np.array_equal(o2.cpu().numpy(), ref2)
+    r.sync()
+    r.close()
