@@ -53,6 +53,7 @@ static double hit_sphere(const rt_sphere& s, V o, V d, double tmin, double close
 struct Ray {
     V o, d;
     double t;  // closest hit (+inf: miss)
+    bool camera = false;
 };
 
 int main(int argc, char** argv) {
@@ -97,7 +98,7 @@ int main(int argc, char** argv) {
                         const double t = hit_sphere(sp[q], o, d, 1e-3, best);
                         if (t < best) { best = t; k = (int)q; }
                     }
-                    rays.push_back({o, d, best});
+                    rays.push_back({o, d, best, b == 0});
                     if (k < 0) break;
                     const rt_sphere& S = sp[k];
                     const V pt = o + d * best;
@@ -213,12 +214,17 @@ int main(int argc, char** argv) {
     const size_t na = bvh.n_always;
     double visits = 0, leaves = 0, wave_steps = 0, wave_leaf = 0, tests = 0;
     std::vector<std::vector<int>> runs(64);
+    const bool skip_camera = std::getenv("SIM_SKIP_CAMERA") != nullptr;
     size_t nw = 0;
     for (size_t w0 = 0; w0 + 64 <= rays.size(); w0 += 64, ++nw) {
         size_t maxleaf = 0;
         for (int l = 0; l < 64; l++) {
             const Ray& R = rays[w0 + l];
             runs[l].clear();
+            if (skip_camera && R.camera) {  // this lane does not walk (its hit comes from elsewhere)
+                runs[l].push_back(0);
+                continue;
+            }
             double closest = INFINITY;
             for (size_t q = 0; q < na; q++) closest = std::min(closest, hit_sphere(sp[bvh.slot_to_sphere[q]], R.o, R.d, 1e-3, closest));
             const float inv[3] = {1.0f / (float)R.d.x, 1.0f / (float)R.d.y, 1.0f / (float)R.d.z};
