@@ -135,7 +135,7 @@ int rt_context_set_scene(rt_context* ctx, const rt_sphere* spheres, size_t n_sph
  * waits for the previous call's work, and scene changes / buffer growth wait for it on the host.
  * A call of at least 2^25 samples on a scene of at least 32 spheres with a camera the context's
  * tree was not built for first rebuilds the BVH from sample rays of that camera (host work,
- * ≈30 ms for the final scene, memoised per process; it waits for the previous call on the host).
+ * ≈16 ms for the final scene, memoised per process; it waits for the previous call on the host).
  * Any tree gives the same bits; this one only walks faster for that camera. */
 int rt_render_rows_async(rt_context* ctx, const rt_camera* cam, uint32_t output_format,
                          uint32_t row0, uint32_t row_step, uint32_t n_rows,

@@ -18,10 +18,14 @@
 #include <cmath>
 #include <limits>
 #include <numeric>
+#include <thread>
 
 namespace rtbvh {
 
 namespace {
+
+constexpr int kParDepth = 2;       // subtrees below nodes at depth <= this are built on their own threads
+constexpr size_t kParMin = 64;     // ... when the node holds at least this many spheres
 
 struct Prim {
     double lo[3], hi[3];  // padded bounds (f64)
@@ -29,14 +33,29 @@ struct Prim {
     uint32_t sphere;      // original index
 };
 
+// a sample segment with its inverse direction (zero components flagged: those slabs test the
+// origin instead)
+struct Seg {
+    double o[3], inv[3], tmax;
+    unsigned zero;  // bit a: d[a] == 0
+};
+
 struct Builder {
+    std::vector<Prim> prim_store;
+    std::vector<Prim>& prims;     // shared with the sub-builders of parallel subtrees (disjoint ranges)
+    std::vector<Seg> seg_store;
+    const std::vector<Seg>& segs; // training segments (read-only once set)
     const std::vector<TrainRay>* train = nullptr;
-    std::vector<Prim> prims;
     std::vector<Node> nodes;
     std::vector<uint32_t> slots;  // leaf slots (after the always-list)
     uint32_t slot_base = 0;
     int max_depth = 0;
     bool failed = false;
+
+    Builder() : prims(prim_store), segs(seg_store) {}
+    // a builder for one subtree of `p`'s tree: same primitives and segments, its own nodes and
+    // leaves (merged back by append())
+    explicit Builder(Builder& p) : prims(p.prims), segs(p.segs), train(p.train), slot_base(p.slot_base) {}
 
     static float down(double x) {
         float f = (float)x;
@@ -81,20 +100,13 @@ struct Builder {
         return ~(int32_t)index;
     }
 
-    // a sample segment with its inverse direction (zero components flagged: those slabs test the
-    // origin instead)
-    struct Seg {
-        double o[3], inv[3], tmax;
-        unsigned zero;  // bit a: d[a] == 0
-    };
-    std::vector<Seg> segs;
     void set_train(const std::vector<TrainRay>* t) {
         train = t;
         if (!t) return;
-        segs.resize(t->size());
+        seg_store.resize(t->size());
         for (size_t i = 0; i < t->size(); i++) {
             const TrainRay& r = (*t)[i];
-            Seg& g = segs[i];
+            Seg& g = seg_store[i];
             g.zero = 0;
             g.tmax = r.tmax;
             for (int a = 0; a < 3; a++) {
@@ -127,24 +139,24 @@ struct Builder {
     // sphere count, but (a near-first walk stops early) much slower than linearly.
     // The left boxes grow with i and the right boxes shrink, so each segment's first entering left
     // split and last entering right split are found by bisection.
-    void ray_costs(size_t b, size_t e, const std::vector<uint32_t>& rays, std::vector<double>& cost) const {
-        const size_t n = e - b;
+    // P: the node's n primitives, sorted on the axis being priced
+    void ray_costs(const Prim* P, size_t n, const std::vector<uint32_t>& rays, std::vector<double>& cost) const {
         std::vector<double> L(6 * n), R(6 * n);  // L[i]: box of the first i prims, R[i]: of prims i..n-1
         double lo[3], hi[3];
-        for (int a = 0; a < 3; a++) { lo[a] = prims[b].lo[a]; hi[a] = prims[b].hi[a]; }
+        for (int a = 0; a < 3; a++) { lo[a] = P[0].lo[a]; hi[a] = P[0].hi[a]; }
         for (size_t i = 1; i < n; i++) {
             for (int a = 0; a < 3; a++) { L[6 * i + a] = lo[a]; L[6 * i + 3 + a] = hi[a]; }
             for (int a = 0; a < 3; a++) {
-                lo[a] = std::min(lo[a], prims[b + i].lo[a]);
-                hi[a] = std::max(hi[a], prims[b + i].hi[a]);
+                lo[a] = std::min(lo[a], P[i].lo[a]);
+                hi[a] = std::max(hi[a], P[i].hi[a]);
             }
         }
-        for (int a = 0; a < 3; a++) { lo[a] = prims[e - 1].lo[a]; hi[a] = prims[e - 1].hi[a]; }
+        for (int a = 0; a < 3; a++) { lo[a] = P[n - 1].lo[a]; hi[a] = P[n - 1].hi[a]; }
         for (size_t i = n - 1; i >= 1; i--) {
             for (int a = 0; a < 3; a++) { R[6 * i + a] = lo[a]; R[6 * i + 3 + a] = hi[a]; }
             for (int a = 0; a < 3; a++) {
-                lo[a] = std::min(lo[a], prims[b + i - 1].lo[a]);
-                hi[a] = std::max(hi[a], prims[b + i - 1].hi[a]);
+                lo[a] = std::min(lo[a], P[i - 1].lo[a]);
+                hi[a] = std::max(hi[a], P[i - 1].hi[a]);
             }
         }
         std::vector<double> first_l(n + 1, 0.0), last_r(n + 1, 0.0);  // histograms
@@ -177,6 +189,21 @@ struct Builder {
         }
     }
 
+    // appends sub-builder c's nodes and leaves after this builder's; returns c's ref `ref` remapped
+    int32_t append(const Builder& c, int32_t ref) {
+        const int32_t noff = (int32_t)nodes.size(), loff = (int32_t)(slots.size() / kLeafMax);
+        auto remap = [&](int32_t r) { return r >= 0 ? r + noff : ~(~r + loff); };
+        for (Node nd : c.nodes) {
+            nd.ref0 = remap(nd.ref0);
+            nd.ref1 = remap(nd.ref1);
+            nodes.push_back(nd);
+        }
+        slots.insert(slots.end(), c.slots.begin(), c.slots.end());
+        max_depth = std::max(max_depth, c.max_depth);
+        failed = failed || c.failed;
+        return remap(ref);
+    }
+
     // returns the ref of the subtree over prims[b, e) at `depth` (root = 1); `rays`: the sample
     // segments that enter this subtree's box
     int32_t build(size_t b, size_t e, int depth, const std::vector<uint32_t>& rays = {}) {
@@ -195,6 +222,7 @@ struct Builder {
         double best_cost = std::numeric_limits<double>::infinity();
         std::vector<double> left_area(n);
         for (int ax = 0; ax < 3; ax++) {
+            if (ax > 0 && !median_only && train && rays.size() >= kMinTrain) break;  // all axes priced at ax 0
             std::sort(prims.begin() + b, prims.begin() + e, [ax](const Prim& x, const Prim& y) {
                 return x.c[ax] < y.c[ax] || (x.c[ax] == y.c[ax] && x.sphere < y.sphere);
             });
@@ -210,14 +238,44 @@ struct Builder {
                 continue;
             }
             if (train && rays.size() >= kMinTrain) {
-                std::vector<double> cost;
-                ray_costs(b, e, rays, cost);
-                for (size_t i = 1; i < n; i++)
-                    if (cost[i] < best_cost) {
-                        best_cost = cost[i];
-                        best_axis = ax;
-                        best_split = b + i;
+                if (ax == 0) {
+                    // price the three axes (on their own threads at the top of the tree, each on a
+                    // copy of the primitives sorted on its axis), then pick in the serial order
+                    std::vector<double> cost[3];
+                    auto price = [&](int a, std::vector<Prim>* copy) {
+                        const Prim* P = &prims[b];
+                        if (copy) {
+                            copy->assign(prims.begin() + b, prims.begin() + e);
+                            std::sort(copy->begin(), copy->end(), [a](const Prim& x, const Prim& y) {
+                                return x.c[a] < y.c[a] || (x.c[a] == y.c[a] && x.sphere < y.sphere);
+                            });
+                            P = copy->data();
+                        }
+                        ray_costs(P, n, rays, cost[a]);
+                    };
+                    if (depth <= kParDepth + 1 && n >= kParMin) {
+                        std::vector<Prim> c1, c2;
+                        std::thread t1(price, 1, &c1), t2(price, 2, &c2);
+                        price(0, nullptr);  // prims[b, e) is sorted on axis 0 here
+                        t1.join();
+                        t2.join();
+                    } else {
+                        price(0, nullptr);
+                        for (int a = 1; a < 3; a++) {
+                            std::sort(prims.begin() + b, prims.begin() + e, [a](const Prim& x, const Prim& y) {
+                                return x.c[a] < y.c[a] || (x.c[a] == y.c[a] && x.sphere < y.sphere);
+                            });
+                            price(a, nullptr);
+                        }
                     }
+                    for (int a = 0; a < 3; a++)
+                        for (size_t i = 1; i < n; i++)
+                            if (cost[a][i] < best_cost) {
+                                best_cost = cost[a][i];
+                                best_axis = a;
+                                best_split = b + i;
+                            }
+                }
                 continue;
             }
             double lo[3], hi[3];
@@ -259,8 +317,20 @@ struct Builder {
             for (uint32_t ri : rays)
                 if (seg_hits(segs[ri], lo, hi)) rays1.push_back(ri);
         }
-        const int32_t r0 = build(b, best_split, depth + 1, rays0);
-        const int32_t r1 = build(best_split, e, depth + 1, rays1);
+        int32_t r0, r1;
+        if (depth <= kParDepth && n >= kParMin) {
+            // the two subtrees are independent (disjoint primitive ranges): build them concurrently
+            // and append them in the serial order (left, then right), so the tree is identical
+            Builder L(*this), R(*this);
+            std::thread t([&] { r0 = L.build(b, best_split, depth + 1, rays0); });
+            r1 = R.build(best_split, e, depth + 1, rays1);
+            t.join();
+            r0 = append(L, r0);
+            r1 = append(R, r1);
+        } else {
+            r0 = build(b, best_split, depth + 1, rays0);
+            r1 = build(best_split, e, depth + 1, rays1);
+        }
         Node& nd = nodes[me];
         set_box(nd.lo0, nd.hi0, b, best_split);
         set_box(nd.lo1, nd.hi1, best_split, e);

@@ -8,6 +8,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <random>
 #include <vector>
 
@@ -87,6 +88,13 @@ static void run(const std::vector<rt_sphere>& s, const char* name, bool trained 
         CHECK(rays.size() >= 3000, "%s: %zu training rays", name, rays.size());
     }
     const rtbvh::Bvh b = rtbvh::build(s.data(), s.size(), ext, trained ? &rays : nullptr);
+    // the builder runs subtrees and axis pricing on threads: the tree must not depend on timing
+    for (int rep = 0; rep < 3; rep++) {
+        const rtbvh::Bvh b2 = rtbvh::build(s.data(), s.size(), ext, trained ? &rays : nullptr);
+        CHECK(b2.ok == b.ok && b2.nodes.size() == b.nodes.size() && b2.slot_to_sphere == b.slot_to_sphere &&
+                  (b.nodes.empty() || std::memcmp(b2.nodes.data(), b.nodes.data(), b.nodes.size() * sizeof(rtbvh::Node)) == 0),
+              "%s: rebuild %d differs", name, rep);
+    }
     CHECK(b.ok, "%s: build failed", name);
     if (!b.ok) return;
     std::vector<uint32_t> seen;

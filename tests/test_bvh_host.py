@@ -11,7 +11,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def test_bvh_builder_invariants(tmp_path, leaf):
     """Builder invariants for the shipped leaf size (2) and the RTZIG_LEAF build knob's values."""
     exe = tmp_path / "test_bvh"
-    subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", f"-DRTZIG_LEAF={leaf}",
+    subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-pthread", f"-DRTZIG_LEAF={leaf}",
                     os.path.join(ROOT, "tests", "cpp", "test_bvh.cpp"),
                     os.path.join(ROOT, "raytracing-with-zig_amd", "csrc", "rt_bvh.cpp"),
                     "-o", str(exe)], check=True)

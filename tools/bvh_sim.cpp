@@ -10,7 +10,7 @@
 //                wave's lanes of the inner steps before the lane's k-th leaf (rays shuffled into
 //                waves, as the persistent kernel mixes paths)
 //
-//   g++ -O2 -std=c++17 tools/bvh_sim.cpp raytracing-with-zig_amd/csrc/rt_bvh.cpp \
+//   g++ -O2 -std=c++17 -pthread tools/bvh_sim.cpp raytracing-with-zig_amd/csrc/rt_bvh.cpp \
 //       raytracing-with-zig_amd/csrc/rt_host.cpp -o /tmp/bvh_sim && /tmp/bvh_sim [stride] [spp] [train_stride (<0: surface rays)] [n_samples: rtbvh::sample_rays]
 #include <algorithm>
 #include <chrono>
