@@ -18,6 +18,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <exception>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -278,11 +279,16 @@ void train_bvh(SceneData& sd, const rt_camera& cam) {
         return;
     }
     const double bound = sd.origin_bound;
-    const rtbvh::Bvh sah = rtbvh::build(sd.spheres.data(), sd.spheres.size(), bound);
-    if (!sah.ok) return;
-    const std::vector<rtbvh::TrainRay> rays =
-        rtbvh::sample_rays(sd.spheres.data(), sd.spheres.size(), cam, sah, kTrainSamples, kTrainSeed);
-    const rtbvh::Bvh tree = rtbvh::build(sd.spheres.data(), sd.spheres.size(), bound, &rays);
+    rtbvh::Bvh sah, tree;
+    try {  // the trained build runs on host threads; if they cannot be had, keep the current tree
+        sah = rtbvh::build(sd.spheres.data(), sd.spheres.size(), bound);
+        if (!sah.ok) return;
+        const std::vector<rtbvh::TrainRay> rays =
+            rtbvh::sample_rays(sd.spheres.data(), sd.spheres.size(), cam, sah, kTrainSamples, kTrainSeed);
+        tree = rtbvh::build(sd.spheres.data(), sd.spheres.size(), bound, &rays);
+    } catch (const std::exception&) {
+        return;
+    }
     if (!tree.ok) return;
     // the kernel stages the tree in LDS when tree + stacks fit a block's 80 KiB (rt_kernel.hip); a
     // trained tree that would not fit where the SAH tree does (or does not build) is not used
