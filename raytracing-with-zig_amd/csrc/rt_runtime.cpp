@@ -242,7 +242,13 @@ void set_tree(SceneData& sd, const rtbvh::Bvh& bvh, double bound) {
 
 // The SAH BVH of sd.spheres, valid for ray origins with |o_i| <= bound.
 void build_bvh(SceneData& sd, double bound) {
-    set_tree(sd, rtbvh::build(sd.spheres.data(), sd.spheres.size(), bound), bound);
+    rtbvh::Bvh bvh;  // ok = false: the linear walk
+    try {            // the builder uses host threads for the top of the tree
+        bvh = rtbvh::build(sd.spheres.data(), sd.spheres.size(), bound);
+    } catch (const std::exception&) {
+        bvh = rtbvh::Bvh{};
+    }
+    set_tree(sd, bvh, bound);
 }
 
 // Do two cameras shoot the same rays (every field getRay / rayColor read except spp and seed)?
