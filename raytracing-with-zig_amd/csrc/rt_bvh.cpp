@@ -12,6 +12,7 @@
 #include "rt_bvh.hpp"
 
 #include <algorithm>
+#include <exception>
 #include <cstdlib>
 #include <utility>
 #include <vector>
@@ -26,6 +27,30 @@ namespace {
 
 constexpr int kParDepth = 2;       // subtrees below nodes at depth <= this are built on their own threads
 constexpr size_t kParMin = 64;     // ... when the node holds at least this many spheres
+
+// f on its own thread while the caller goes on; join() rethrows what f threw, and the destructor
+// joins, so no exception leaves a thread running or escapes one
+struct Task {
+    std::exception_ptr err;
+    std::thread t;
+    template <class F>
+    explicit Task(F f) : t([this, f] {
+        try {
+            f();
+        } catch (...) {
+            err = std::current_exception();
+        }
+    }) {}
+    Task(const Task&) = delete;
+    Task& operator=(const Task&) = delete;
+    void join() {
+        if (t.joinable()) t.join();
+        if (err) std::rethrow_exception(err);
+    }
+    ~Task() {
+        if (t.joinable()) t.join();
+    }
+};
 
 struct Prim {
     double lo[3], hi[3];  // padded bounds (f64)
@@ -255,7 +280,8 @@ struct Builder {
                     };
                     if (depth <= kParDepth + 1 && n >= kParMin) {
                         std::vector<Prim> c1, c2;
-                        std::thread t1(price, 1, &c1), t2(price, 2, &c2);
+                        Task t1([&] { price(1, &c1); });
+                        Task t2([&] { price(2, &c2); });
                         price(0, nullptr);  // prims[b, e) is sorted on axis 0 here
                         t1.join();
                         t2.join();
@@ -322,7 +348,7 @@ struct Builder {
             // the two subtrees are independent (disjoint primitive ranges): build them concurrently
             // and append them in the serial order (left, then right), so the tree is identical
             Builder L(*this), R(*this);
-            std::thread t([&] { r0 = L.build(b, best_split, depth + 1, rays0); });
+            Task t([&] { r0 = L.build(b, best_split, depth + 1, rays0); });
             r1 = R.build(best_split, e, depth + 1, rays1);
             t.join();
             r0 = append(L, r0);
