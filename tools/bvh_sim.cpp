@@ -215,6 +215,9 @@ int main(int argc, char** argv) {
     double visits = 0, leaves = 0, wave_steps = 0, wave_leaf = 0, tests = 0;
     std::vector<std::vector<int>> runs(64);
     const bool skip_camera = std::getenv("SIM_SKIP_CAMERA") != nullptr;
+    const bool skip_dead = std::getenv("SIM_SKIP_DEAD") != nullptr;  // pop past dead stack entries for free
+    const bool skip_leaf_only = std::getenv("SIM_SKIP_DEAD_LEAF_ONLY") != nullptr;  // ... only after a leaf round
+    double dead = 0;
     size_t nw = 0;
     for (size_t w0 = 0; w0 + 64 <= rays.size(); w0 += 64, ++nw) {
         size_t maxleaf = 0;
@@ -240,9 +243,23 @@ int main(int argc, char** argv) {
                 tn = t0;
                 return t0 <= t1;
             };
-            std::vector<int32_t> stack;
+            std::vector<std::pair<int32_t, float>> stack;  // (ref, entry distance of its box)
             int32_t cur = 0;
             int run = 0;
+            // pop, optionally skipping entries whose box starts beyond the current closest (dead)
+            auto pop = [&](int32_t& out, bool after_leaf) {
+                while (!stack.empty()) {
+                    const auto e = stack.back();
+                    stack.pop_back();
+                    if (e.second > (float)closest * (1 + 1e-6f)) {
+                        dead++;
+                        if (skip_dead && (after_leaf || !skip_leaf_only)) continue;
+                    }
+                    out = e.first;
+                    return true;
+                }
+                return false;
+            };
             while (true) {
                 if (cur >= 0) {
                     const rtbvh::Node& nd = bvh.nodes[cur];
@@ -252,14 +269,12 @@ int main(int argc, char** argv) {
                     const bool h0 = box(nd.lo0, nd.hi0, n0), h1 = box(nd.lo1, nd.hi1, n1);
                     if (h0 && h1) {
                         const bool f0 = n0 <= n1;
-                        stack.push_back(f0 ? nd.ref1 : nd.ref0);
+                        stack.push_back({f0 ? nd.ref1 : nd.ref0, f0 ? n1 : n0});
                         cur = f0 ? nd.ref0 : nd.ref1;
                     } else if (h0 || h1) {
                         cur = h0 ? nd.ref0 : nd.ref1;
                     } else {
-                        if (stack.empty()) break;
-                        cur = stack.back();
-                        stack.pop_back();
+                        if (!pop(cur, false)) break;
                     }
                 } else {
                     runs[l].push_back(run);
@@ -272,9 +287,7 @@ int main(int argc, char** argv) {
                         tests++;
                         closest = std::min(closest, hit_sphere(sp[k], R.o, R.d, 1e-3, closest));
                     }
-                    if (stack.empty()) break;
-                    cur = stack.back();
-                    stack.pop_back();
+                    if (!pop(cur, true)) break;
                 }
             }
             runs[l].push_back(run);
@@ -290,7 +303,7 @@ int main(int argc, char** argv) {
     }
     const double nr = (double)nw * 64;
     std::printf("{\"nodes\": %zu, \"depth\": %d, \"n_always\": %zu, \"visits_per_ray\": %.4f, \"leaves_per_ray\": %.4f, "
-                "\"leaf_tests_per_ray\": %.4f, \"wave_inner_steps\": %.3f, \"wave_leaf_rounds\": %.3f}\n",
-                bvh.nodes.size(), bvh.depth, na, visits / nr, leaves / nr, tests / nr, wave_steps / nw, wave_leaf / nw);
+                "\"leaf_tests_per_ray\": %.4f, \"wave_inner_steps\": %.3f, \"wave_leaf_rounds\": %.3f, \"dead_pops_per_ray\": %.4f}\n",
+                bvh.nodes.size(), bvh.depth, na, visits / nr, leaves / nr, tests / nr, wave_steps / nw, wave_leaf / nw, dead / nr);
     return 0;
 }
