@@ -34,7 +34,7 @@ extern "C" {
 /* ---- status codes ---------------------------------------------------------------------------- */
 typedef enum rt_status {
     RT_OK = 0,
-    RT_ERR_INVALID = -1,   /* bad argument (n==0, W/H/spp==0, negative radius, bad material...) */
+    RT_ERR_INVALID = -1,   /* bad argument (n==0, W/H/spp==0, bad material, non-finite camera...) */
     RT_ERR_HIP = -2,       /* HIP runtime error (message in rt_last_error) */
     RT_ERR_NO_DEVICE = -3, /* no gfx950 device visible / extension not built for it */
     RT_ERR_CAPACITY = -4,  /* too large: > 2^24 spheres, or a launch with >= 2^32 work units */

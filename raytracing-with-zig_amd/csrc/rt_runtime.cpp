@@ -151,6 +151,16 @@ int validate_camera(const rt_camera* c) {
         rt_set_last_error("image must have fewer than 2^32 pixels");
         return RT_ERR_INVALID;
     }
+    // the camera vectors must be finite (the reference would render NaN pixels; here a NaN center
+    // would also defeat the BVH's origin bound); t_max may be +inf, never NaN
+    const double* v[6] = {c->center, c->pixel0, c->du, c->dv, c->defocus_disk_u, c->defocus_disk_v};
+    bool finite = std::isfinite(c->defocus_angle) && std::isfinite(c->t_min) && !std::isnan(c->t_max);
+    for (const double* x : v)
+        for (int a = 0; a < 3; a++) finite = finite && std::isfinite(x[a]);
+    if (!finite) {
+        rt_set_last_error("camera vectors, defocus_angle and t_min must be finite (t_max may be +inf)");
+        return RT_ERR_INVALID;
+    }
     return RT_OK;
 }
 

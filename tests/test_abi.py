@@ -89,6 +89,18 @@ def test_invalid_arguments_fail_without_gpu_work():
     rc = lib.rt_render(C.byref(cam), (rtzig.RtSphere * 1)(rtzig.RtSphere(radius=1.0)), 1,
                        C.byref(opts), C.c_void_p(1))
     assert rc == abi.RT_ERR_INVALID
+    # non-finite camera vectors are rejected (t_max = +inf stays legal)
+    cam.samples_per_pixel = 1
+    cam.t_max = float("inf")
+    cam.center[1] = float("nan")
+    rc = lib.rt_render(C.byref(cam), (rtzig.RtSphere * 1)(rtzig.RtSphere(radius=1.0)), 1,
+                       C.byref(opts), C.c_void_p(1))
+    assert rc == abi.RT_ERR_INVALID and b"finite" in lib.rt_last_error()
+    cam.center[1] = 0.0
+    cam.t_min = float("inf")
+    rc = lib.rt_render(C.byref(cam), (rtzig.RtSphere * 1)(rtzig.RtSphere(radius=1.0)), 1,
+                       C.byref(opts), C.c_void_p(1))
+    assert rc == abi.RT_ERR_INVALID
 
 
 def test_single_hip_runtime_per_process():
