@@ -301,6 +301,127 @@ int main(int argc, char** argv) {
             wave_steps += m;
         }
     }
+    // ---- lockstep model of one wave (SIM_LOCKSTEP): all lanes advance together; with SIM_STEAL a
+    // lane whose walk is over takes the oldest stack entry of the lane with the deepest stack and
+    // walks that subtree for the same ray (closest shared instantly: an optimistic bound) ----
+    double ls_steps = 0, ls_leaf = 0, ls_steals = 0;
+    size_t ls_waves = 0;
+    if (std::getenv("SIM_LOCKSTEP")) {
+        const bool steal = std::getenv("SIM_STEAL") != nullptr;
+        // helpers cull with the owner's closest as it was when they stole (no sharing until the end)
+        const bool snap = std::getenv("SIM_STEAL_SNAPSHOT") != nullptr;
+        const size_t min_victim = std::getenv("SIM_STEAL_MIN") ? (size_t)std::atoi(std::getenv("SIM_STEAL_MIN")) : 1;
+        const bool steal_top = std::getenv("SIM_STEAL_TOP") != nullptr;  // take the newest entry instead of the oldest
+        const int max_helpers = std::getenv("SIM_STEAL_MAXH") ? std::atoi(std::getenv("SIM_STEAL_MAXH")) : 64;  // per ray, over the walk
+        const int32_t kDoneRef = INT32_MIN;
+        for (size_t w0 = 0; w0 + 64 <= rays.size(); w0 += 64, ++ls_waves) {
+            double cl[64], lc[64];  // per-ray closest (shared); per-lane copies (snapshot mode)
+            float org[64][3], inv[64][3];
+            int ray[64];
+            int32_t cur[64];
+            std::vector<int32_t> st[64];
+            for (int l = 0; l < 64; l++) {
+                const Ray& R = rays[w0 + l];
+                cl[l] = INFINITY;
+                for (size_t q = 0; q < na; q++) cl[l] = std::min(cl[l], hit_sphere(sp[bvh.slot_to_sphere[q]], R.o, R.d, 1e-3, cl[l]));
+                org[l][0] = (float)R.o.x; org[l][1] = (float)R.o.y; org[l][2] = (float)R.o.z;
+                inv[l][0] = 1.0f / (float)R.d.x; inv[l][1] = 1.0f / (float)R.d.y; inv[l][2] = 1.0f / (float)R.d.z;
+                ray[l] = l;
+                lc[l] = cl[l];
+                cur[l] = 0;
+                if (skip_camera && R.camera) cur[l] = kDoneRef;
+            }
+            auto boxt = [&](int l, int r, const float* lo, const float* hi, float& tn) {
+                float t0 = 1e-3f, t1 = (float)(snap ? lc[l] : cl[r]) * (1 + 1e-6f);
+                for (int a = 0; a < 3; a++) {
+                    float ta = (lo[a] - org[r][a]) * inv[r][a], tb = (hi[a] - org[r][a]) * inv[r][a];
+                    if (ta > tb) std::swap(ta, tb);
+                    t0 = std::max(t0, ta);
+                    t1 = std::min(t1, tb);
+                }
+                tn = t0;
+                return t0 <= t1;
+            };
+            auto pop = [&](int l) {
+                if (st[l].empty()) { cur[l] = kDoneRef; return; }
+                cur[l] = st[l].back();
+                st[l].pop_back();
+            };
+            int helpers[64] = {0};
+            auto try_steal = [&](int l) {  // l is idle: take the oldest entry of the deepest stack
+                int v = -1;
+                size_t best = 0;
+                for (int m = 0; m < 64; m++)
+                    if (m != l && st[m].size() >= min_victim && st[m].size() > best && helpers[ray[m]] < max_helpers) {
+                        best = st[m].size();
+                        v = m;
+                    }
+                if (v < 0) return;
+                helpers[ray[v]]++;
+                if (steal_top) {
+                    cur[l] = st[v].back();
+                    st[v].pop_back();
+                } else {
+                    cur[l] = st[v].front();
+                    st[v].erase(st[v].begin());
+                }
+                ray[l] = ray[v];
+                lc[l] = lc[v];
+                ls_steals++;
+            };
+            while (true) {
+                // inner phase
+                while (true) {
+                    bool any = false;
+                    for (int l = 0; l < 64; l++) {
+                        if (cur[l] < 0) continue;
+                        any = true;
+                        const rtbvh::Node& nd = bvh.nodes[cur[l]];
+                        float n0, n1;
+                        const int r = ray[l];
+                        const bool h0 = boxt(l, r, nd.lo0, nd.hi0, n0), h1 = boxt(l, r, nd.lo1, nd.hi1, n1);
+                        if (h0 && h1) {
+                            const bool f0 = n0 <= n1;
+                            st[l].push_back(f0 ? nd.ref1 : nd.ref0);
+                            cur[l] = f0 ? nd.ref0 : nd.ref1;
+                        } else if (h0 || h1) {
+                            cur[l] = h0 ? nd.ref0 : nd.ref1;
+                        } else {
+                            pop(l);
+                        }
+                    }
+                    if (!any) break;
+                    ls_steps++;
+                    if (steal)
+                        for (int l = 0; l < 64; l++)
+                            if (cur[l] == kDoneRef) try_steal(l);
+                }
+                bool leaf = false;
+                for (int l = 0; l < 64; l++) leaf = leaf || (cur[l] != kDoneRef);
+                if (!leaf) break;
+                ls_leaf++;
+                for (int l = 0; l < 64; l++) {
+                    if (cur[l] == kDoneRef) continue;
+                    const Ray& R = rays[w0 + ray[l]];
+                    const size_t base = na + (size_t)rtbvh::kLeafMax * (size_t)(~cur[l]);
+                    for (int u = 0; u < rtbvh::kLeafMax; u++) {
+                        const uint32_t k = bvh.slot_to_sphere[base + u];
+                        if (k == rtbvh::kSentinel) continue;
+                        const double t = hit_sphere(sp[k], R.o, R.d, 1e-3, snap ? lc[l] : cl[ray[l]]);
+                        lc[l] = std::min(lc[l], t);
+                        cl[ray[l]] = std::min(cl[ray[l]], t);
+                    }
+                    pop(l);
+                }
+                if (steal)
+                    for (int l = 0; l < 64; l++)
+                        if (cur[l] == kDoneRef) try_steal(l);
+            }
+        }
+        std::fprintf(stderr, "lockstep%s: wave steps %.3f, leaf rounds %.3f, steals per wave %.2f\n",
+                     steal ? "+steal" : "", ls_steps / ls_waves, ls_leaf / ls_waves, ls_steals / ls_waves);
+    }
+
     const double nr = (double)nw * 64;
     std::printf("{\"nodes\": %zu, \"depth\": %d, \"n_always\": %zu, \"visits_per_ray\": %.4f, \"leaves_per_ray\": %.4f, "
                 "\"leaf_tests_per_ray\": %.4f, \"wave_inner_steps\": %.3f, \"wave_leaf_rounds\": %.3f, \"dead_pops_per_ray\": %.4f}\n",
