@@ -312,6 +312,9 @@ int main(int argc, char** argv) {
         const bool snap = std::getenv("SIM_STEAL_SNAPSHOT") != nullptr;
         const size_t min_victim = std::getenv("SIM_STEAL_MIN") ? (size_t)std::atoi(std::getenv("SIM_STEAL_MIN")) : 1;
         const bool steal_top = std::getenv("SIM_STEAL_TOP") != nullptr;  // take the newest entry instead of the oldest
+        // helpers only traverse: a leaf a helper reaches is pushed onto its owner's stack (the owner
+        // tests it later with its own f64 ray); a lane with a helper out does not help others
+        const bool trav_only = std::getenv("SIM_STEAL_TRAVERSE_ONLY") != nullptr;
         const int max_helpers = std::getenv("SIM_STEAL_MAXH") ? std::atoi(std::getenv("SIM_STEAL_MAXH")) : 64;  // per ray, over the walk
         const int32_t kDoneRef = INT32_MIN;
         for (size_t w0 = 0; w0 + 64 <= rays.size(); w0 += 64, ++ls_waves) {
@@ -348,7 +351,11 @@ int main(int argc, char** argv) {
                 st[l].pop_back();
             };
             int helpers[64] = {0};
+            int out[64] = {0};   // helpers currently working for lane l's ray
+            int owner[64];
+            for (int l = 0; l < 64; l++) owner[l] = l;
             auto try_steal = [&](int l) {  // l is idle: take the oldest entry of the deepest stack
+                if (trav_only && out[l] > 0) return;  // keeps its stack free for returned leaves
                 int v = -1;
                 size_t best = 0;
                 for (int m = 0; m < 64; m++)
@@ -367,6 +374,8 @@ int main(int argc, char** argv) {
                 }
                 ray[l] = ray[v];
                 lc[l] = lc[v];
+                owner[l] = owner[v];
+                out[owner[v]]++;
                 ls_steals++;
             };
             while (true) {
@@ -392,6 +401,20 @@ int main(int argc, char** argv) {
                     }
                     if (!any) break;
                     ls_steps++;
+                    if (trav_only)  // helpers hand their leaves to the owner and keep traversing
+                        for (int l = 0; l < 64; l++) {
+                            if (owner[l] == l) continue;
+                            if (cur[l] < 0 && cur[l] != kDoneRef) {
+                                const int o = owner[l];
+                                if (cur[o] == kDoneRef) cur[o] = cur[l]; else st[o].push_back(cur[l]);
+                                pop(l);
+                            }
+                            if (cur[l] == kDoneRef && st[l].empty()) {  // subtree finished
+                                out[owner[l]]--;
+                                owner[l] = l;
+                                ray[l] = l;
+                            }
+                        }
                     if (steal)
                         for (int l = 0; l < 64; l++)
                             if (cur[l] == kDoneRef) try_steal(l);
