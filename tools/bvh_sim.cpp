@@ -304,7 +304,7 @@ int main(int argc, char** argv) {
     // ---- lockstep model of one wave (SIM_LOCKSTEP): all lanes advance together; with SIM_STEAL a
     // lane whose walk is over takes the oldest stack entry of the lane with the deepest stack and
     // walks that subtree for the same ray (closest shared instantly: an optimistic bound) ----
-    double ls_steps = 0, ls_leaf = 0, ls_steals = 0;
+    double ls_steps = 0, ls_leaf = 0, ls_steals = 0, ls_batches = 0;
     size_t ls_waves = 0;
     if (std::getenv("SIM_LOCKSTEP")) {
         const bool steal = std::getenv("SIM_STEAL") != nullptr;
@@ -315,6 +315,8 @@ int main(int argc, char** argv) {
         // helpers only traverse: a leaf a helper reaches is pushed onto its owner's stack (the owner
         // tests it later with its own f64 ray); a lane with a helper out does not help others
         const bool trav_only = std::getenv("SIM_STEAL_TRAVERSE_ONLY") != nullptr;
+        const int max_batches = std::getenv("SIM_STEAL_MAXB") ? std::atoi(std::getenv("SIM_STEAL_MAXB")) : 1 << 30;  // per wave walk
+        const int min_idle = std::getenv("SIM_STEAL_MIN_IDLE") ? std::atoi(std::getenv("SIM_STEAL_MIN_IDLE")) : 1;  // idle lanes to start a batch
         const int max_helpers = std::getenv("SIM_STEAL_MAXH") ? std::atoi(std::getenv("SIM_STEAL_MAXH")) : 64;  // per ray, over the walk
         const int32_t kDoneRef = INT32_MIN;
         for (size_t w0 = 0; w0 + 64 <= rays.size(); w0 += 64, ++ls_waves) {
@@ -351,6 +353,7 @@ int main(int argc, char** argv) {
                 st[l].pop_back();
             };
             int helpers[64] = {0};
+            int batches = 0;
             int out[64] = {0};   // helpers currently working for lane l's ray
             int owner[64];
             for (int l = 0; l < 64; l++) owner[l] = l;
@@ -415,9 +418,14 @@ int main(int argc, char** argv) {
                                 ray[l] = l;
                             }
                         }
-                    if (steal)
+                    int idle = 0;
+                    for (int l = 0; l < 64; l++) idle += cur[l] == kDoneRef;
+                    if (steal && batches < max_batches && idle >= min_idle) {
+                        const double before = ls_steals;
                         for (int l = 0; l < 64; l++)
                             if (cur[l] == kDoneRef) try_steal(l);
+                        if (ls_steals > before) { ls_batches++; batches++; }
+                    }
                 }
                 bool leaf = false;
                 for (int l = 0; l < 64; l++) leaf = leaf || (cur[l] != kDoneRef);
@@ -436,13 +444,19 @@ int main(int argc, char** argv) {
                     }
                     pop(l);
                 }
-                if (steal)
+                int idle2 = 0;
+                for (int l = 0; l < 64; l++) idle2 += cur[l] == kDoneRef;
+                if (steal && batches < max_batches && idle2 >= min_idle) {
+                    const double before = ls_steals;
                     for (int l = 0; l < 64; l++)
                         if (cur[l] == kDoneRef) try_steal(l);
+                    if (ls_steals > before) { ls_batches++; batches++; }
+                }
             }
         }
-        std::fprintf(stderr, "lockstep%s: wave steps %.3f, leaf rounds %.3f, steals per wave %.2f\n",
-                     steal ? "+steal" : "", ls_steps / ls_waves, ls_leaf / ls_waves, ls_steals / ls_waves);
+        std::fprintf(stderr, "lockstep%s: wave steps %.3f, leaf rounds %.3f, steals per wave %.2f in %.2f batches\n",
+                     steal ? "+steal" : "", ls_steps / ls_waves, ls_leaf / ls_waves, ls_steals / ls_waves,
+                     ls_batches / ls_waves);
     }
 
     const double nr = (double)nw * 64;
