@@ -319,7 +319,8 @@ int main(int argc, char** argv) {
         const int min_idle = std::getenv("SIM_STEAL_MIN_IDLE") ? std::atoi(std::getenv("SIM_STEAL_MIN_IDLE")) : 1;  // idle lanes to start a batch
         const int max_helpers = std::getenv("SIM_STEAL_MAXH") ? std::atoi(std::getenv("SIM_STEAL_MAXH")) : 64;  // per ray, over the walk
         const int32_t kDoneRef = INT32_MIN;
-        for (size_t w0 = 0; w0 + 64 <= rays.size(); w0 += 64, ++ls_waves) {
+        const int walkers = std::getenv("SIM_WALKERS") ? std::atoi(std::getenv("SIM_WALKERS")) : 64;  // lanes with a ray
+        for (size_t w0 = 0; w0 + 64 <= rays.size(); w0 += walkers, ++ls_waves) {
             double cl[64], lc[64];  // per-ray closest (shared); per-lane copies (snapshot mode)
             float org[64][3], inv[64][3];
             int ray[64];
@@ -335,6 +336,7 @@ int main(int argc, char** argv) {
                 lc[l] = cl[l];
                 cur[l] = 0;
                 if (skip_camera && R.camera) cur[l] = kDoneRef;
+                if (l >= walkers) cur[l] = kDoneRef;  // no path to walk this iteration: a helper from the start
             }
             auto boxt = [&](int l, int r, const float* lo, const float* hi, float& tn) {
                 float t0 = 1e-3f, t1 = (float)(snap ? lc[l] : cl[r]) * (1 + 1e-6f);
