@@ -39,11 +39,11 @@ constexpr uint32_t kMaxLdsSpheres = 2048;  // 64 KiB of LDS geometry; above this
 // tiles: (tile, chunk) units would either be large (a long drain) or so many that the claim
 // counter's rate (≈88 claims per µs) bounds the launch.
 // ------------------------------------------------------------------------------------------------
-constexpr uint32_t kUnitS = 16;  // samples per unit of the main chunks (ring slot size)
-constexpr uint32_t kSlots = 4;   // units a wave holds at once (16 x 4 measured best)
+constexpr uint32_t kUnitS = 48;  // samples per unit of the main chunks (ring slot size)
+constexpr uint32_t kSlots = 2;   // units a wave holds at once (48 x 2 measured best)
 constexpr uint32_t kSlotMask = (1u << kSlots) - 1;
 constexpr uint32_t kRingSlotDoubles = kUnitS * 64 * 3;
-constexpr uint32_t kRingWaveDoubles = kSlots * kRingSlotDoubles;  // 96 KiB of f64 per wave
+constexpr uint32_t kRingWaveDoubles = kSlots * kRingSlotDoubles;  // 144 KiB of f64 per wave
 // claim counters (zeroed per launch): ring mode ctr[0]; direct mode one per queue segment, each on
 // its own 128-B line, ctr[kCtrStride * seg]; then the error word ctr[kErrWord]
 constexpr uint32_t kSegs = 8;

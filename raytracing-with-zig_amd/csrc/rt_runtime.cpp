@@ -4,8 +4,8 @@
 // One render of rows = ONE persistent launch of the sample kernel.  It accumulates every pixel's
 // samples in sample order itself (rt_kernel.h "Work units", rt_units.h): work units of 64 pixels x
 // a chunk of samples, wave-private rings for the colors of unfinished units, and per-pixel running
-// sums handed from wave to wave behind a per-tile flag.  The workspace is fixed: the rings (96 KiB
-// per resident wave, ≈ 0.8 GB on 256 CUs) plus 24 B of running sum per pixel and 4 B of flag per
+// sums handed from wave to wave behind a per-tile flag.  The workspace is fixed: the rings (144 KiB
+// per wave slot, ≈ 1.2 GB on 256 CUs) plus 24 B of running sum per pixel and 4 B of flag per
 // 64 pixels — independent of spp, and no reduce pass.
 //
 // rt_render() keeps one cached context per device for the life of the process (SURVEY §8(b):

@@ -11,14 +11,17 @@ pytestmark = pytest.mark.gpu
 
 
 def test_too_many_units_is_refused():
-    """16384 x 16384 pixels x 20000 spp: 4.2 M tiles x ~1250 chunks > 2^32 units -> RT_ERR_CAPACITY,
-    returned before any buffer is allocated or kernel launched (the context stays usable)."""
-    big = rtzig.final_scene_camera(width=16384, aspect_ratio=1.0, spp=20000)
+    """16384 x 16384 pixels x 4 M spp: 4.2 M tiles x ~83 000 chunks (of up to kUnitS = 48 samples)
+    > 2^32 units -> RT_ERR_CAPACITY, returned before any buffer is allocated or kernel launched (the
+    context stays usable).  The output buffer is full-size, so a regression that launched anyway
+    would run long, never write out of bounds."""
+    big = rtzig.final_scene_camera(width=16384, aspect_ratio=1.0, spp=4_000_000)
     r = rtzig.DeviceRenderer(0)
     r.set_scene(big.scene.world)
-    dummy = torch.zeros(3, dtype=torch.float64, device="cuda:0")
+    full = torch.empty((big.height, big.width, 3), dtype=torch.float64, device="cuda:0")
     with pytest.raises(RtError) as e:
-        r.render_rows_async(big.cam, dummy.data_ptr())
+        r.render_rows_async(big.cam, full.data_ptr())
+    del full
     assert e.value.code == rtzig.abi.RT_ERR_CAPACITY
     small = rtzig.final_scene_camera(width=32, aspect_ratio=1.0, spp=2)
     out = torch.zeros((32, 32, 3), dtype=torch.float64, device="cuda:0")

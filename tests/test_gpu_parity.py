@@ -396,9 +396,9 @@ def test_kernel_times_total_accumulates():
 
 
 @pytest.mark.parametrize("mode", ["ring", "direct"])
-@pytest.mark.parametrize("spp", [1, 2, 3, 15, 16, 17, 31, 33, 47, 100])
+@pytest.mark.parametrize("spp", [1, 2, 3, 15, 16, 17, 31, 33, 47, 48, 49, 95, 97, 100])
 def test_unit_schedule_sample_counts_bit_exact(oracle, spp, mode, monkeypatch):
-    """Every chunk schedule shape of the unit scheduler (rt_kernel.h "Work units": chunks of up to 16
+    """Every chunk schedule shape of the unit scheduler (rt_kernel.h "Work units": chunks of up to kUnitS = 48
     samples, shrinking towards the end, rt_schedule.hpp) on an image whose pixel count is not a
     multiple of 64 (a partial last tile), in both modes: the ring's in-kernel ordered accumulation
     and direct mode's stored samples + reduce pass must give oracle B's bits."""
