@@ -110,7 +110,7 @@ typedef struct rt_options {
  * `pixel_stride` doubles (first 3 are r,g,b); RGB8: W*H*3 bytes.  Blocks the calling thread.
  * The library keeps one device context per GPU for the life of the process (created on first use,
  * on parallel host threads): a later call on the same sphere list re-uploads and rebuilds nothing.
- * Its workspace is fixed per device: ≈ 0.8 GB of wave rings plus 24 B per pixel (the kernel
+ * Its workspace is fixed per device: ≈ 1.2 GB of wave rings plus 24 B per pixel (the kernel
  * accumulates every pixel's samples in order itself); launches whose samples fit 2 GiB instead
  * store them (at most 2 GiB) and sum them in order in a second pass.  Calls are serialised by
  * an internal lock.                                                                               */
