@@ -5,8 +5,9 @@
 // launch ends in a long drain tail with most lanes idle; but small units cost lane utilisation (a
 // ring slot frees only when the slowest of its paths ends).  So chunk sizes shrink towards the end
 // of the launch: built backwards from the last chunk (1 sample), a chunk may hold S samples only if
-// S <= ratio * (samples after it), ratio = pixels / (8 * resident lanes), and S <= kUnitS (a ring
-// slot).  The divisor 8 is measured (config 4, rows 0::N, N = 1, 4, 8: 2, 3, 6, 8, 16 all slower).
+// S <= ratio * (samples after it), ratio = pixels / (6 * resident lanes), and S <= kUnitS (a ring
+// slot).  The divisor is measured: 8 with 16-sample units (config 4, rows 0::N, N = 1, 4, 8: 2, 3,
+// 6, 16 slower), 6 with the 48 x 2 ring (4, 8, 12, 16 slower).
 // The full frame gets kUnitS-sample chunks up to the last few samples; a rank's rows of an 8-GPU
 // job taper off over the last ~250 samples.
 #pragma once
@@ -17,9 +18,11 @@
 
 namespace rtk {
 
+constexpr double kSchedDiv = 6.0;  // drain divisor: ratio = pixels / (kSchedDiv * resident lanes)
+
 // s0 of every chunk plus a final entry == spp (chunk k covers samples [s0[k], s0[k + 1])).
 inline std::vector<uint32_t> chunk_schedule(uint32_t spp, uint64_t pixels, uint64_t lanes, uint32_t max_chunk) {
-    const double ratio = (double)pixels / (8.0 * (double)std::max<uint64_t>(lanes, 1));
+    const double ratio = (double)pixels / (kSchedDiv * (double)std::max<uint64_t>(lanes, 1));
     std::vector<uint32_t> rev;
     uint32_t after = 0;
     while (after < spp) {

@@ -2,7 +2,7 @@
 // chunk_range): for every spp and launch size the chunks tile [0, spp) contiguously in order, never
 // exceed a ring slot (kUnitS), shrink monotonically towards the end (the first chunk is the
 // remainder and may be smaller), end with a 1-sample chunk, and
-// obey the drain bound S <= max(1, pixels / (8 lanes) * samples_after).  Built with hipcc (host code
+// obey the drain bound S <= max(1, pixels / (kSchedDiv lanes) * samples_after).  Built with hipcc (host code
 // only; no GPU needed).
 #include <cstdio>
 #include <cstdlib>
@@ -17,7 +17,7 @@ static int check(uint32_t spp, uint64_t pixels, uint64_t lanes) {
         std::printf("spp %u pixels %llu: bad table ends (%zu chunks)\n", spp, (unsigned long long)pixels, n_chunks);
         return 1;
     }
-    const double ratio = (double)pixels / (8.0 * (double)lanes);
+    const double ratio = (double)pixels / (rtk::kSchedDiv * (double)lanes);
     uint32_t prev = 0xffffffffu;
     for (size_t k = 0; k < n_chunks; ++k) {
         const uint32_t n = t[k + 1] - t[k], after = spp - t[k + 1];
