@@ -77,7 +77,10 @@ __device__ __forceinline__ void chunk_range(const UnitArgs& u, uint32_t k, uint3
 }
 
 constexpr uint32_t kPad = 4;               // sphere list padded to a multiple of this (sentinels)
-constexpr int kRuvTrips = 3;  // randomUnitVec rejection trips per loop iteration (path_loop; 2, 4 slower)
+#ifndef RTZIG_RUV_TRIPS
+#define RTZIG_RUV_TRIPS 3
+#endif
+constexpr int kRuvTrips = RTZIG_RUV_TRIPS;  // randomUnitVec rejection trips per loop iteration (path_loop; 2, 4 slower)
 constexpr const char* kDefaultVariant = "smem_u4";  // see variant_choice() in rt_kernel.hip
 
 // Geometry walked by every lane for every ray: 32 B, one LDS broadcast pair per sphere.
