@@ -41,7 +41,7 @@ int main() {
             if (check(spp, px, lanes)) return 1;
     for (uint64_t px : sizes)
         if (check(10000, px, lanes)) return 1;
-    // the bench launch: 960000 pixels at 500 spp keeps 16-sample chunks up to the last few samples
+    // the bench launch: 960000 pixels at 500 spp keeps kUnitS-sample chunks up to the last few samples
     const std::vector<uint32_t> big = rtk::chunk_schedule(500, 1200 * 800, lanes, rtk::kUnitS);
     if (big.size() - 1 > 500 / rtk::kUnitS + 12) { std::printf("bench launch: %zu chunks\n", big.size() - 1); return 1; }
     std::printf("OK\n");
