@@ -9,6 +9,9 @@
 //   wave steps   while-while inner steps per 64-ray wave: sum over segments k of the max over the
 //                wave's lanes of the inner steps before the lane's k-th leaf (rays shuffled into
 //                waves, as the persistent kernel mixes paths)
+// Wave models (environment): SIM_LOCKSTEP (+ SIM_STEAL*: walk splitting across lanes),
+// SIM_REFETCH=K (+ SIM_REFETCH_P): lanes that finish their walk take a new segment after each leaf
+// round once K of them are done.
 //
 //   g++ -O2 -std=c++17 -pthread tools/bvh_sim.cpp raytracing-with-zig_amd/csrc/rt_bvh.cpp \
 //       raytracing-with-zig_amd/csrc/rt_host.cpp -o /tmp/bvh_sim && /tmp/bvh_sim [stride] [spp] [train_stride (<0: surface rays)] [n_samples: rtbvh::sample_rays]
@@ -459,6 +462,112 @@ int main(int argc, char** argv) {
         std::fprintf(stderr, "lockstep%s: wave steps %.3f, leaf rounds %.3f, steals per wave %.2f in %.2f batches\n",
                      steal ? "+steal" : "", ls_steps / ls_waves, ls_leaf / ls_waves, ls_steals / ls_waves,
                      ls_batches / ls_waves);
+    }
+
+    // ---- dynamic fetch (SIM_REFETCH=K): one 64-lane wave streams through all the rays; after a
+    // leaf round, once at least K lanes have finished their walk, each of them takes the next ray
+    // (in the kernel: shade the finished segment and start the next one inside the walk loop, one
+    // wave-uniform shading block per refetch batch).  Reported per 64 rays, to compare with the
+    // lockstep model's per-wave figures. ----
+    if (std::getenv("SIM_REFETCH")) {
+        const int min_done = std::atoi(std::getenv("SIM_REFETCH"));
+        // SIM_REFETCH_P: chance that a lane leaving a shading batch has a segment to walk (the
+        // kernel's other lanes wait on rejection trips or a refill: ~40 of 64 walk per iteration)
+        const double p_ready = std::getenv("SIM_REFETCH_P") ? std::atof(std::getenv("SIM_REFETCH_P")) : 1.0;
+        std::mt19937_64 prng(7);
+        std::uniform_real_distribution<double> PU(0.0, 1.0);
+        const int32_t kDoneRef = INT32_MIN;
+        double cl[64];
+        float org[64][3], inv[64][3];
+        int32_t cur[64];
+        std::vector<int32_t> st[64];
+        size_t next = 0, started = 0;
+        double steps = 0, leafr = 0, batches = 0, lane_steps = 0;
+        auto start = [&](int l) {
+            if (next >= rays.size()) { cur[l] = kDoneRef; return; }
+            const Ray& R = rays[next++];
+            ++started;
+            cl[l] = INFINITY;
+            for (size_t q = 0; q < na; q++) cl[l] = std::min(cl[l], hit_sphere(sp[bvh.slot_to_sphere[q]], R.o, R.d, 1e-3, cl[l]));
+            org[l][0] = (float)R.o.x; org[l][1] = (float)R.o.y; org[l][2] = (float)R.o.z;
+            inv[l][0] = 1.0f / (float)R.d.x; inv[l][1] = 1.0f / (float)R.d.y; inv[l][2] = 1.0f / (float)R.d.z;
+            st[l].clear();
+            cur[l] = 0;
+        };
+        std::vector<size_t> rid(64);
+        for (int l = 0; l < 64; l++) { rid[l] = next; start(l); }
+        auto boxt = [&](int l, const float* lo, const float* hi, float& tn) {
+            float t0 = 1e-3f, t1 = (float)cl[l] * (1 + 1e-6f);
+            for (int a = 0; a < 3; a++) {
+                float ta = (lo[a] - org[l][a]) * inv[l][a], tb = (hi[a] - org[l][a]) * inv[l][a];
+                if (ta > tb) std::swap(ta, tb);
+                t0 = std::max(t0, ta);
+                t1 = std::min(t1, tb);
+            }
+            tn = t0;
+            return t0 <= t1;
+        };
+        auto pop = [&](int l) {
+            if (st[l].empty()) { cur[l] = kDoneRef; return; }
+            cur[l] = st[l].back();
+            st[l].pop_back();
+        };
+        while (true) {
+            bool live = false;
+            for (int l = 0; l < 64; l++) live = live || cur[l] != kDoneRef;
+            if (!live && next >= rays.size()) break;
+            while (true) {  // inner phase
+                int act = 0;
+                for (int l = 0; l < 64; l++) {
+                    if (cur[l] < 0) continue;
+                    ++act;
+                    const rtbvh::Node& nd = bvh.nodes[cur[l]];
+                    float n0, n1;
+                    const bool h0 = boxt(l, nd.lo0, nd.hi0, n0), h1 = boxt(l, nd.lo1, nd.hi1, n1);
+                    if (h0 && h1) {
+                        const bool f0 = n0 <= n1;
+                        st[l].push_back(f0 ? nd.ref1 : nd.ref0);
+                        cur[l] = f0 ? nd.ref0 : nd.ref1;
+                    } else if (h0 || h1) {
+                        cur[l] = h0 ? nd.ref0 : nd.ref1;
+                    } else {
+                        pop(l);
+                    }
+                }
+                if (!act) break;
+                ++steps;
+                lane_steps += act;
+            }
+            bool leaf = false;
+            for (int l = 0; l < 64; l++) leaf = leaf || cur[l] != kDoneRef;
+            if (leaf) {
+                ++leafr;
+                for (int l = 0; l < 64; l++) {
+                    if (cur[l] == kDoneRef) continue;
+                    const Ray& R = rays[rid[l]];
+                    const size_t base = na + (size_t)rtbvh::kLeafMax * (size_t)(~cur[l]);
+                    for (int u = 0; u < rtbvh::kLeafMax; u++) {
+                        const uint32_t k = bvh.slot_to_sphere[base + u];
+                        if (k == rtbvh::kSentinel) continue;
+                        cl[l] = std::min(cl[l], hit_sphere(sp[k], R.o, R.d, 1e-3, cl[l]));
+                    }
+                    pop(l);
+                }
+            }
+            int done = 0;
+            for (int l = 0; l < 64; l++) done += cur[l] == kDoneRef;
+            const bool all_done = done == 64;
+            if (next < rays.size() && (done >= min_done || all_done)) {
+                ++batches;
+                for (int l = 0; l < 64; l++)
+                    if (cur[l] == kDoneRef && PU(prng) < p_ready) { rid[l] = next; start(l); }
+            } else if (all_done) {
+                break;
+            }
+        }
+        const double per = 64.0 / (double)started;
+        std::fprintf(stderr, "refetch K=%d: per 64 rays: wave steps %.3f, leaf rounds %.3f, shading batches %.3f; lane util %.3f\n",
+                     min_done, steps * per, leafr * per, batches * per, lane_steps / (64.0 * steps));
     }
 
     const double nr = (double)nw * 64;
