@@ -219,10 +219,16 @@ struct LinearWalker {
     const GeoRec* __restrict__ geo;
     uint32_t n_pad;
     uint32_t n_real;
+    static constexpr bool kCanSuspend = false;
+    struct State {};
     template <class PR>
     __device__ __forceinline__ int operator()(const Ray& r, double t_min, double t_max, double* t, PR& pr) const {
         pr.tests(n_real);
         return world_hit<U>(geo, n_pad, r, t_min, t_max, t);
+    }
+    template <bool kSusp, class PR>
+    __device__ __forceinline__ int run(const Ray& r, double t_min, double t_max, double* t, PR& pr, State&, bool) const {
+        return (*this)(r, t_min, t_max, t, pr);
     }
 };
 
@@ -255,6 +261,15 @@ __device__ __forceinline__ int32_t sel_mask(int32_t f, int32_t t, uint64_t m) {
 //   t_k = root1 if t_min < root1, else root2 if t_min < root2   (sphere.zig:38-41),
 // and it wins iff t_k < closest, or t_k == closest and k is lower (the linear scan's first-wins).
 constexpr int32_t kDone = INT32_MIN;  // walk finished (stack entry 0)
+// Dynamic fetch (RTZIG_REFETCH_K > 0): after a leaf round, once at least K lanes of the wave are
+// free (walk over, or not walking), the walk returns kSuspended for the lanes still walking; they
+// keep their walk state (BvhWalker::State, the stack stays in LDS) and resume in the next
+// iteration, while the free lanes shade and start their next segment.
+#ifndef RTZIG_REFETCH_K
+#define RTZIG_REFETCH_K 56
+#endif
+constexpr int kRefetchK = RTZIG_REFETCH_K;
+constexpr int kSuspended = -2;
 typedef float f2 __attribute__((ext_vector_type(2)));
 // {b.x * m.x + a.x, b.y * m.x + a.x}: v_pk_fma_f32 with the second and third operands' low halves
 // broadcast to the high lane (op_sel_hi:[1,0,0]); their high halves are never read
@@ -396,15 +411,38 @@ struct BvhWalker {
         }
     }
 
+    static constexpr bool kCanSuspend = true;
+    struct State {  // a suspended walk (dynamic fetch)
+        int32_t cur;
+        int32_t* top;
+        double closest;
+        uint32_t best;
+        bool found;
+    };
     template <class PR>
     __device__ __forceinline__ int operator()(const Ray& r, double t_min, double t_max, double* t_hit, PR& pr) const {
+        State s;
+        return run<false>(r, t_min, t_max, t_hit, pr, s, false);
+    }
+    template <bool kSusp, class PR>
+    __device__ __forceinline__ int run(const Ray& r, double t_min, double t_max, double* t_hit, PR& pr, State& st,
+                                       const bool resume) const {
         const double a = len_sq(r.dir);
         double closest = t_max;
         uint32_t best = 0;
         bool found = false;
+        if constexpr (kSusp) {
+            if (resume) {
+                closest = st.closest;
+                best = st.best;
+                found = st.found;
+            }
+        }
         const LeafFilter lfilt = LeafFilter::make(a, t_min);
         const RayDiv ad(a);
-        if (n_always <= 4) {
+        if (kSusp && resume) {
+            // the always-list and the far-origin check ran when this walk started
+        } else if (n_always <= 4) {
             // the common case (the ground and up to three big spheres), unrolled so that closest /
             // best / found are not loop-carried through a runtime-bounded loop
             // n_always is re-read from the kernarg segment at each test (a held copy of each
@@ -416,7 +454,7 @@ struct BvhWalker {
         } else {
             for (uint32_t q = 0; q < n_always; ++q) test_always(q, r, a, ad, t_min, lfilt, closest, best, found, pr);
         }
-        pr.tests(n_always);
+        if (!(kSusp && resume)) pr.tests(n_always);
 
         // f32 ray for the conservative slab tests (error budget: rt_bvh.cpp)
         const float ox = (float)r.orig.x, oy = (float)r.orig.y, oz = (float)r.orig.z;
@@ -444,8 +482,9 @@ struct BvhWalker {
         // scan, exact) and skips the tree.  Only rays leaving an unboundable always-list sphere get
         // there, so the common path pays one compare and one ballot per ray.  (A NaN origin fails
         // every sphere test anyway; the max drops it.)
-        const bool far = __builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(ox), __builtin_fabsf(oy)), __builtin_fabsf(oz)) >
-                         origin_bound;
+        const bool far = !(kSusp && resume) &&
+                         __builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(ox), __builtin_fabsf(oy)), __builtin_fabsf(oz)) >
+                             origin_bound;
         if (__builtin_expect(__ballot(far) != 0, 0)) {
             if (far) {
                 double t;
@@ -470,6 +509,12 @@ struct BvhWalker {
         // pushed far children; a pop reads entry sp, so popping the empty stack yields kDone
         int32_t* top = stack;  // this lane's stack entry sp (entry i at stack[i * kBlockBvh])
         int32_t cur = far ? kDone : 0;  // root
+        if constexpr (kSusp) {
+            if (resume) {
+                top = st.top;
+                cur = st.cur;
+            }
+        }
         // while-while (Aila & Laine 2009): every lane advances through internal nodes until it
         // holds a leaf (or is done); then the lanes with a leaf test its spheres together, so the
         // f64 leaf work runs with most lanes active instead of whenever any one lane hits a leaf.
@@ -597,6 +642,21 @@ struct BvhWalker {
                 cur = *top;  // pop (entry 0: kDone)
                 top -= kBlockBvh;
             }
+            if constexpr (kSusp) {
+                // wave-uniform: enough free lanes to make a shading batch worthwhile
+                const uint64_t walking = __ballot(cur != kDone);
+                if (walking != 0 && 64 - __popcll(walking) >= kRefetchK) break;
+            }
+        }
+        if constexpr (kSusp) {
+            if (cur != kDone) {
+                st.cur = cur;
+                st.top = top;
+                st.closest = closest;
+                st.best = best;
+                st.found = found;
+                return kSuspended;
+            }
         }
         *t_hit = closest;
         return found ? (int)best : -1;
@@ -629,6 +689,9 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
     bool dpend = false;  // camera ray waiting for its defocus-disk sample (camera_start)
     double sc_fuzz = 0;
     v3 sc_nrm = mk(0, 0, 0), sc_refl = mk(0, 0, 0);
+    constexpr bool kSusp = kRefetchK > 0 && Walker::kCanSuspend;
+    typename Walker::State ws;  // a suspended walk (dynamic fetch, kSusp only)
+    bool susp = false;          // this lane's walk is suspended
     uint64_t rays = 0, nsamples = 0;
     Prof<kProf> pr;
     uint64_t cyc_refill = 0, cyc_walk = 0, cyc_shade = 0, cyc_trips = 0;  // wave-uniform (kProf only)
@@ -745,7 +808,7 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
                 done = true;  // too many bounces -> black (camera.zig:181)
             } else {
                 double t;
-                ++rays;
+                if (!susp) ++rays;
                 uint64_t v0 = 0, t0 = 0;
                 if constexpr (kProf) { v0 = pr.n_visits; t0 = pr.n_tests; }
                 // The walk is a chain of dependent LDS reads: raised issue priority lets a wave whose
@@ -754,12 +817,19 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
                 // raised priority everywhere but the trip loop was slower).  The shading that follows
                 // (dependent loads of the hit sphere's records) runs at priority 1 (chapter 13 -1.3%).
                 __builtin_amdgcn_s_setprio(2);
-                const int k = walk(r, p.t_min, p.t_max, &t, pr);
+                int k;
+                if constexpr (kSusp) {
+                    k = walk.template run<true>(r, p.t_min, p.t_max, &t, pr, ws, susp);
+                    susp = k == kSuspended;
+                } else {
+                    k = walk(r, p.t_min, p.t_max, &t, pr);
+                }
                 __builtin_amdgcn_s_setprio(1);
                 if constexpr (kProf) {
                     if (bounce == 0) { pr.cam_visits += pr.n_visits - v0; pr.cam_tests += pr.n_tests - t0; }
                 }
                 if constexpr (kProf) t_walk1 = __builtin_amdgcn_s_memtime();
+                if (!susp) {  // a suspended walk resumes next iteration; nothing to shade yet
                 // Three branches below need a unit vector: the sky (unit(ray.dir).y), the
                 // dielectric (unit(ray.dir)) and the metal (unit(reflect(ray.dir, n))).  Each is a
                 // correctly rounded sqrt and division, and a wave executes every branch some lane
@@ -821,6 +891,7 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
                     r.orig = pt;
                     r.dir = dir;
                     ++bounce;
+                }
                 }
             }
         }
