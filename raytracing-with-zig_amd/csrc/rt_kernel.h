@@ -39,8 +39,14 @@ constexpr uint32_t kMaxLdsSpheres = 2048;  // 64 KiB of LDS geometry; above this
 // tiles: (tile, chunk) units would either be large (a long drain) or so many that the claim
 // counter's rate (≈88 claims per µs) bounds the launch.
 // ------------------------------------------------------------------------------------------------
-constexpr uint32_t kUnitS = 48;  // samples per unit of the main chunks (ring slot size)
-constexpr uint32_t kSlots = 2;   // units a wave holds at once (48 x 2 measured best)
+#ifndef RTZIG_UNIT_S
+#define RTZIG_UNIT_S 48
+#endif
+#ifndef RTZIG_SLOTS
+#define RTZIG_SLOTS 2
+#endif
+constexpr uint32_t kUnitS = RTZIG_UNIT_S;  // samples per unit of the main chunks (ring slot size)
+constexpr uint32_t kSlots = RTZIG_SLOTS;   // units a wave holds at once (48 x 2 measured best)
 constexpr uint32_t kSlotMask = (1u << kSlots) - 1;
 constexpr uint32_t kRingSlotDoubles = kUnitS * 64 * 3;
 constexpr uint32_t kRingWaveDoubles = kSlots * kRingSlotDoubles;  // 144 KiB of f64 per wave
