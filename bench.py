@@ -7,6 +7,12 @@ reference src/camera.zig:123-145) on the final random-sphere scene — BASELINE.
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 
+Without a launcher (WORLD_SIZE unset), --gpus N > 1 starts the N ranks itself: N fresh worker
+processes (torch.multiprocessing spawn, before anything in this process touches the GPU), each
+joining the process group on 127.0.0.1.  A rank count the devices cannot serve (nccl: one device
+per rank) or a --gpus that disagrees with WORLD_SIZE is an error (non-zero exit), never a silent
+1-GPU run.
+
 A step = one full frame: every rank renders its rows (one HIP kernel launch via the C ABI, inputs
 resident in HBM) and the rows are gathered to rank 0 over RCCL.  The image is fixed, so N>1 is
 strong scaling.  Rank 0 prints ONE JSON line.
@@ -117,7 +123,7 @@ def dropin(cam, device):
     return times
 
 
-def main():
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
@@ -132,15 +138,69 @@ def main():
     ap.add_argument("--no-dropin", action="store_true", help="skip the rt_render drop-in measurement")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL over xGMI, the product) or gloo (rehearsal: several ranks on one GPU)")
-    args = ap.parse_args()
+    ap.add_argument("--launch-check", action="store_true",
+                    help="start the ranks and join the process group, print one line, render nothing")
+    return ap.parse_args(argv)
 
+
+def _free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def _worker(rank, argv, world, port):
+    """One rank started by main() (no external launcher): the env a launcher would set, then run()."""
+    os.environ.update({"RANK": str(rank), "LOCAL_RANK": str(rank), "WORLD_SIZE": str(world),
+                       "LOCAL_WORLD_SIZE": str(world), "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
+    run(parse_args(argv))
+
+
+def main():
+    argv = sys.argv[1:]
+    args = parse_args(argv)
+    if args.gpus < 1:
+        sys.exit(f"bench.py: --gpus must be >= 1 (got {args.gpus})")
+    if "WORLD_SIZE" in os.environ:
+        world = int(os.environ["WORLD_SIZE"])
+        if world != args.gpus:
+            sys.exit(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks")
+        run(args)
+    elif args.gpus == 1:
+        run(args)
+    else:
+        # no launcher: start the ranks here.  spawn = fresh interpreters; this process has not
+        # touched the GPU and does not exec anything itself.
+        import torch.multiprocessing as mp
+        try:
+            mp.spawn(_worker, args=(argv, args.gpus, _free_port()), nprocs=args.gpus, join=True)
+        except Exception as e:  # a rank failed: its traceback is on stderr
+            sys.exit(f"bench.py: a rank failed ({type(e).__name__}: {e})")
+
+
+def run(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if args.gpus != world and world > 1:
-        log(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
-    # gloo rehearsal: ranks may share a device (local rank modulo the visible device count)
+    if args.launch_check:
+        # rank plumbing only (CPU tests): join a gloo group, agree on the world size, print it
+        if world > 1:
+            dist.init_process_group("gloo", rank=rank, world_size=world)
+            t = torch.tensor([1])
+            dist.all_reduce(t)
+            n = int(t.item())
+            dist.destroy_process_group()
+        else:
+            n = 1
+        if rank == 0:
+            print(json.dumps({"launch_check": True, "n_gpus": n, "gpus_arg": args.gpus}), flush=True)
+        return
     ndev = torch.cuda.device_count()
+    if args.dist_backend == "nccl" and ndev < world:
+        raise SystemExit(f"bench.py: {world} ranks over nccl need {world} visible GPUs, found {ndev} "
+                         "(use --dist-backend gloo to rehearse several ranks on one GPU)")
+    # gloo rehearsal: ranks may share a device (local rank modulo the visible device count)
     local_dev = local if args.dist_backend == "nccl" else local % max(1, ndev)
     torch.cuda.set_device(local_dev)
     dev = torch.device("cuda", local_dev)
@@ -168,16 +228,17 @@ def main():
     torch.cuda.synchronize()
     init_ms = (time.perf_counter() - t_init) * 1e3
 
+    def gather():
+        if args.dist_backend == "gloo" and world > 1:
+            return rdist.gather_image(out.cpu(), H, rank, world)  # gloo gathers host tensors
+        return rdist.gather_image(out, H, rank, world)
+
     def frame(stats_ptr=None):
         if n_rows:
             renderer.render_rows_async(cam.cam, out.data_ptr(), row0=row0, row_step=step,
                                        n_rows=n_rows, output=args.output, d_stats_ptr=stats_ptr,
                                        stream_ptr=stream.cuda_stream)
-        if args.dist_backend == "gloo" and world > 1:
-            img = rdist.gather_image(out.cpu(), H, rank, world)  # gloo gathers host tensors
-        else:
-            img = rdist.gather_image(out, H, rank, world)
-        return img
+        return gather()
 
     # the first frame also pays the one-time BVH rebuild from sample rays of this camera (DESIGN.md
     # §5 "Ray-driven tree"): its wall time is reported as a fixed cost
@@ -222,6 +283,29 @@ def main():
     elapsed_max = float(t.item())
     kname = renderer.kernel_name()  # the timed (parity) kernel, before the fast-mode frames
     k_sum, r_sum, n_launch = renderer.kernel_times_total() if n_rows else (0.0, 0.0, 0)
+    renderer.sync()  # raises if a wave of any timed frame gave up on a hand-off (sticky error word)
+    # N > 1: the gather alone, K times, bracketed like the timed region (the frame's other part)
+    coll_dev = dev if args.dist_backend == "nccl" else "cpu"
+    gather_ms = 0.0
+    if world > 1:
+        dist.barrier()
+        torch.cuda.synchronize()
+        tg = time.perf_counter()
+        for _ in range(args.steps):
+            gather()
+        torch.cuda.synchronize()
+        dist.barrier()
+        gather_ms = (time.perf_counter() - tg) / args.steps * 1e3
+    mine = torch.tensor([float(rank), float(n_rows), k_sum / args.steps, r_sum / args.steps, gather_ms,
+                         elapsed / args.steps * 1e3], dtype=torch.float64, device=coll_dev)
+    if world > 1:
+        every = [torch.zeros_like(mine) for _ in range(world)]
+        dist.all_gather(every, mine)
+    else:
+        every = [mine]
+    per_rank = [{"rank": int(v[0]), "rows": int(v[1]), "kernel_ms_per_frame": round(float(v[2]), 3),
+                 "reduce_ms_per_frame": round(float(v[3]), 3), "gather_ms": round(float(v[4]), 3),
+                 "ms_per_step": round(float(v[5]), 3)} for v in (x.cpu() for x in every)]
     st = stats.cpu().tolist()
     rays_per_frame = st[0] / max(1, args.steps)
     samples_per_frame = st[1] / max(1, args.steps)
@@ -243,7 +327,7 @@ def main():
                 "note": "RT_PRECISION_F32 fast mode (huge spheres in f64), statistical parity only; "
                         "not the headline value"}
         renderer.set_precision("f64")
-    renderer.sync()  # raises if a wave reported a hand-off timeout (never expected)
+    renderer.sync()
     renderer.close()
 
     if rank == 0:
@@ -281,7 +365,7 @@ def main():
             "metric": METRIC,
             "value": round(value, 3),
             "unit": "Msamples/s",
-            "n_gpus": world,
+            "n_gpus": dist.get_world_size() if world > 1 else 1,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(frame_ms, 3),
@@ -337,6 +421,7 @@ def main():
                             ("direct mode (small launch): every sample's 24-B color stored and read back once by "
                              f"the reduce pass, {n_rows * W * spp * 48 / 1e9:.2f} GB per frame"),
             },
+            "ranks": per_rank,
             "rays_per_sample": round(rays_per_frame / max(1, samples_per_frame), 4),
             "fixed_costs_ms": {"context_and_scene_upload": round(init_ms, 2),
                                "first_frame_incl_bvh_training": round(first_ms, 2) if first_ms else None},

@@ -54,7 +54,8 @@ struct SceneData {
     std::vector<rtk::GeoRec> ageo;
     std::vector<uint32_t> asid;
     uint32_t n_nodes = 0, n_leaves = 0, n_always = 0, depth = 0;
-    bool trained = false;  // the tree was built from sample rays of camera `view` (train_bvh)
+    bool trained = false;      // the tree was built from sample rays of camera `view` (train_bvh)
+    bool train_tried = false;  // train_bvh ran for `view` (trained or not: a failure is not retried)
     rt_camera view{};
 };
 
@@ -69,6 +70,8 @@ constexpr size_t kTrainMinSpheres = 32;
 constexpr size_t kTrainSamples = RTZIG_TRAIN_SAMPLES;  // build knob
 constexpr uint64_t kTrainSeed = 0x7261792d74726565ull;
 constexpr uint32_t kLinearMaxSpheres = 8;    // scenes this small walk the list (use_bvh)
+constexpr const char* kStallMsg =
+    "render kernel: a wave gave up waiting for a running-sum hand-off (no unit finalised for 40 s)";
 
 }  // namespace
 
@@ -204,6 +207,7 @@ rtk::GeoRec geo_of(const rt_sphere* s) {
 // Sets sd's device tree from `bvh` (built for ray origins with |o_i| <= bound; rt_kernel.h layout).
 void set_tree(SceneData& sd, const rtbvh::Bvh& bvh, double bound) {
     sd.trained = false;
+    sd.train_tried = false;
     // byte-offset refs must fit int32 (and stay clear of the walk's INT32_MIN "done" marker)
     const bool fits = bvh.nodes.size() * sizeof(rtk::BvhNode) < (1ull << 30) &&
                       bvh.slot_to_sphere.size() / rtk::kLeafBvh * sizeof(rtk::BvhLeaf) < (1ull << 30);
@@ -283,29 +287,22 @@ bool want_train(const SceneData& sd, uint64_t samples) {
 // Rebuilds sd's tree from sample rays of `cam` (rtbvh::sample_rays over the SAH tree, then the
 // ray-driven build).  The result depends only on (spheres, origin bound, view), so it is memoised
 // process-wide: rt_render's devices and later calls reuse it.  Any valid tree returns the same
-// bits (rt_bvh.hpp); this one only visits fewer nodes for this camera's rays.
-void train_bvh(SceneData& sd, const rt_camera& cam) {
-    static std::mutex mu;
-    static SceneData memo;
-    std::lock_guard<std::mutex> lock(mu);
-    if (memo.trained && same_view(memo.view, cam) && memo.origin_bound == sd.origin_bound &&
-        memo.spheres.size() == sd.spheres.size() &&
-        std::memcmp(memo.spheres.data(), sd.spheres.data(), sd.spheres.size() * sizeof(rt_sphere)) == 0) {
-        sd = memo;
-        return;
-    }
+// bits (rt_bvh.hpp); this one only visits fewer nodes for this camera's rays.  A training that
+// fails or is rejected (builder exception, no tree, LDS budget) keeps the current tree and is
+// memoised too (train_tried), so later launches of the same view do not quiesce and retry it.
+bool try_train(SceneData& sd, const rt_camera& cam) {
     const double bound = sd.origin_bound;
     rtbvh::Bvh sah, tree;
     try {  // the trained build runs on host threads; if they cannot be had, keep the current tree
         sah = rtbvh::build(sd.spheres.data(), sd.spheres.size(), bound);
-        if (!sah.ok) return;
+        if (!sah.ok) return false;
         const std::vector<rtbvh::TrainRay> rays =
             rtbvh::sample_rays(sd.spheres.data(), sd.spheres.size(), cam, sah, kTrainSamples, kTrainSeed);
         tree = rtbvh::build(sd.spheres.data(), sd.spheres.size(), bound, &rays);
     } catch (const std::exception&) {
-        return;
+        return false;
     }
-    if (!tree.ok) return;
+    if (!tree.ok) return false;
     // the kernel stages the tree in LDS when tree + stacks fit a block's 80 KiB (rt_kernel.hip); a
     // trained tree that would not fit where the SAH tree does (or does not build) is not used
     auto lds_bytes = [](const SceneData& t) {
@@ -314,14 +311,33 @@ void train_bvh(SceneData& sd, const rt_camera& cam) {
     };
     SceneData sah_sd = sd;
     set_tree(sah_sd, sah, bound);
-    set_tree(sd, tree, bound);
-    if (!sd.bvh_ok || (lds_bytes(sd) > rtk::kLdsSceneBudget && lds_bytes(sah_sd) <= rtk::kLdsSceneBudget)) {
-        sd = sah_sd;
+    SceneData tr = sd;
+    set_tree(tr, tree, bound);
+    if (!tr.bvh_ok || (lds_bytes(tr) > rtk::kLdsSceneBudget && lds_bytes(sah_sd) <= rtk::kLdsSceneBudget)) {
+        if (sah_sd.bvh_ok) sd = sah_sd;
+        return false;
+    }
+    sd = tr;
+    return true;
+}
+
+void train_bvh(SceneData& sd, const rt_camera& cam) {
+    static std::mutex mu;
+    static SceneData memo;
+    static bool memo_valid = false;
+    std::lock_guard<std::mutex> lock(mu);
+    if (memo_valid && same_view(memo.view, cam) && memo.origin_bound == sd.origin_bound &&
+        memo.spheres.size() == sd.spheres.size() &&
+        std::memcmp(memo.spheres.data(), sd.spheres.data(), sd.spheres.size() * sizeof(rt_sphere)) == 0) {
+        sd = memo;
         return;
     }
-    sd.trained = true;
+    const bool ok = try_train(sd, cam);
+    sd.trained = ok;
+    sd.train_tried = true;
     sd.view = cam;
     memo = sd;
+    memo_valid = true;
 }
 
 // Device records + BVH of a sphere list (validated by the caller).
@@ -385,9 +401,18 @@ int upload(rt_context* ctx, T** dptr, size_t* bytes, const std::vector<T>& v) {
     return RT_OK;
 }
 
-int upload_bvh(rt_context* ctx) {
+// After a failed upload the context holds no scene: its device buffers may have been freed or
+// half-written, so the host copy must not vouch for them (a cached rt_render context would compare
+// same_spheres() as true and launch on freed memory).  The next set_scene / rt_render re-uploads.
+void invalidate_scene(rt_context* ctx) {
+    ctx->scene = SceneData{};
+    ctx->n_spheres = 0;
+    ctx->bvh = rtk::BvhArgs{};
+}
+
+int upload_bvh_buffers(rt_context* ctx) {
     const SceneData& sd = ctx->scene;
-    if (!sd.bvh_ok) return RT_OK;
+    ctx->bvh = rtk::BvhArgs{};  // the buffers below may be reallocated
     int rc = quiesce(ctx);
     if (!rc) rc = upload(ctx, &ctx->d_nodes, &ctx->nodes_bytes, sd.nodes);
     if (!rc) rc = upload(ctx, &ctx->d_leaves, &ctx->leaves_bytes, sd.leaves);
@@ -395,6 +420,18 @@ int upload_bvh(rt_context* ctx) {
     if (!rc) rc = upload(ctx, &ctx->d_always_sid, &ctx->always_sid_bytes, sd.asid);
     if (rc) return rc;
     HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    return RT_OK;
+}
+
+// Uploads ctx->scene's tree (any failure leaves the context without a scene: invalidate_scene).
+int upload_bvh(rt_context* ctx) {
+    if (!ctx->scene.bvh_ok) return RT_OK;
+    const int rc = upload_bvh_buffers(ctx);
+    if (rc) {
+        invalidate_scene(ctx);
+        return rc;
+    }
+    const SceneData& sd = ctx->scene;
     rtk::BvhArgs& b = ctx->bvh;
     b = rtk::BvhArgs{};
     b.nodes = ctx->d_nodes;
@@ -415,7 +452,8 @@ int upload_bvh(rt_context* ctx) {
 }
 
 // Uploads a host scene to the context's device (a copy stays on the host side of the context).
-int upload_scene(rt_context* ctx, const SceneData& sd) {
+// The host copy is committed only once every device buffer holds it.
+int upload_scene_buffers(rt_context* ctx, const SceneData& sd) {
     HIP_CHECK(hipSetDevice(ctx->device));
     int rc = quiesce(ctx);
     if (rc) return rc;
@@ -433,9 +471,16 @@ int upload_scene(rt_context* ctx, const SceneData& sd) {
     HIP_CHECK(hipMemcpyAsync(ctx->d_geo, sd.geo.data(), n_pad * sizeof(rtk::GeoRec), hipMemcpyHostToDevice, ctx->stream));
     HIP_CHECK(hipMemcpyAsync(ctx->d_mat, sd.mat.data(), n * sizeof(rtk::MatRec), hipMemcpyHostToDevice, ctx->stream));
     HIP_CHECK(hipStreamSynchronize(ctx->stream));
-    ctx->n_spheres = (uint32_t)n;
+    return RT_OK;
+}
+
+int upload_scene(rt_context* ctx, const SceneData& sd) {
+    invalidate_scene(ctx);  // nothing on the device vouches for the old scene any more
+    const int rc = upload_scene_buffers(ctx, sd);
+    if (rc) return rc;
     ctx->scene = sd;
-    return upload_bvh(ctx);
+    ctx->n_spheres = (uint32_t)sd.mat.size();
+    return upload_bvh(ctx);  // invalidates again on failure
 }
 
 // Walk selection: RTZIG_KERNEL names a linear variant (lds_u4, smem_u4) or "bvh"; default: the
@@ -576,10 +621,13 @@ int rt_context_sync(rt_context* ctx) {
     HIP_CHECK(hipSetDevice(ctx->device));
     int rc = quiesce(ctx);
     if (rc || !ctx->d_ctr) return rc;
+    // the error word is sticky across launches: it reports a failure of ANY render since the last
+    // report, and is cleared once reported
     unsigned long long err = 0;
     HIP_CHECK(hipMemcpy(&err, ctx->d_ctr + rtk::kErrWord, sizeof err, hipMemcpyDeviceToHost));
     if (err) {
-        rt_set_last_error("render kernel: a wave timed out waiting for a running-sum hand-off");
+        HIP_CHECK(hipMemset(ctx->d_ctr + rtk::kErrWord, 0, sizeof err));
+        rt_set_last_error(kStallMsg);
         return RT_ERR_HIP;
     }
     return RT_OK;
@@ -618,7 +666,7 @@ int rt_render_rows_async(rt_context* ctx, const rt_camera* cam, uint32_t output_
     }
     // large launches walk a tree trained on this camera's rays (same bits, fewer node visits)
     if (want_train(ctx->scene, (uint64_t)n_rows * cam->image_width * cam->samples_per_pixel) &&
-        !(ctx->scene.trained && same_view(ctx->scene.view, *cam))) {
+        !(ctx->scene.train_tried && same_view(ctx->scene.view, *cam))) {
         rc = quiesce(ctx);  // the previous render may still walk the old tree
         if (rc) return rc;
         train_bvh(ctx->scene, *cam);
@@ -664,6 +712,8 @@ int rt_render_rows_async(rt_context* ctx, const rt_camera* cam, uint32_t output_
     if (!rc && !ctx->d_ctr) {
         size_t cb = 0;
         rc = ensure_buffer(ctx, (void**)&ctx->d_ctr, &cb, rtk::kCtrBytes);
+        // the sticky error word starts clear; launches zero only the counters before it
+        if (!rc) HIP_CHECK(hipMemset(ctx->d_ctr, 0, rtk::kCtrBytes));
     }
     if (rc) return rc;
     ua.ring = direct ? nullptr : ctx->d_ring;
@@ -695,7 +745,7 @@ int rt_render_rows_async(rt_context* ctx, const rt_camera* cam, uint32_t output_
     }
     // a previous render of this context on another stream may still use the buffers
     if (ctx->done_valid && ctx->done_stream != s) HIP_CHECK(hipStreamWaitEvent(s, ctx->done, 0));
-    HIP_CHECK(hipMemsetAsync(ctx->d_ctr, 0, rtk::kCtrBytes, s));
+    HIP_CHECK(hipMemsetAsync(ctx->d_ctr, 0, rtk::kCtrLaunchBytes, s));  // not the sticky error word
     if (!direct) HIP_CHECK(hipMemsetAsync(ctx->d_flags, 0, flag_bytes, s));
     const bool bvh = use_bvh(ctx);
     rtk::KernelParams p = make_params(cam, row0, row_step, n_rows, ctx->n_spheres);
@@ -785,16 +835,52 @@ const char* rt_kernel_name(rt_context* ctx) { return ctx ? ctx->last_kernel : "r
 namespace {
 
 std::mutex g_cache_mu;             // guards g_cache and serialises rt_render calls
-std::vector<rt_context*> g_cache;  // one context per device ordinal (created on first use)
+std::vector<rt_context*> g_cache;  // one context per logical device ordinal (created on first use)
+
+// rt_render's logical devices: ordinal g runs on physical device map[g].  Normally the identity
+// over the visible devices.  Test hook RTZIG_DEVICE_MAP=p0,p1,... (physical ordinals, repeats
+// allowed) gives rt_render that many logical devices, so the multi-device branch (contexts created
+// on host threads, one stream each, row interleave, un-interleave, stats sum) runs on a 1-GPU host
+// exactly as on an 8-GPU one: RTZIG_DEVICE_MAP=0,0,0 is three contexts on GPU 0.
+int device_map(std::vector<int>& map) {
+    int count = 0;
+    HIP_CHECK(hipGetDeviceCount(&count));
+    if (count <= 0) { rt_set_last_error("no HIP device"); return RT_ERR_NO_DEVICE; }
+    map.clear();
+    const char* e = std::getenv("RTZIG_DEVICE_MAP");
+    if (!e || !*e) {
+        for (int d = 0; d < count; d++) map.push_back(d);
+        return RT_OK;
+    }
+    const char* p = e;
+    while (*p) {
+        char* endp = nullptr;
+        const long d = std::strtol(p, &endp, 10);
+        if (endp == p || d < 0 || d >= count) {
+            rt_set_last_error(std::string("RTZIG_DEVICE_MAP: bad entry in \"") + e + "\" (" + std::to_string(count) +
+                              " visible devices)");
+            return RT_ERR_NO_DEVICE;
+        }
+        map.push_back((int)d);
+        p = endp;
+        if (*p == ',') ++p;
+    }
+    return RT_OK;
+}
 
 // Gets (creating if needed) the cached contexts of devices [first, first + G) and makes each hold
 // `spheres`: contexts are created on parallel host threads; the scene is built on the host once
 // per call at most and uploaded only where it differs.
-int cached_contexts(int first, int G, const rt_sphere* spheres, size_t n, std::vector<rt_context*>& out) {
+int cached_contexts(const std::vector<int>& map, int first, int G, const rt_sphere* spheres, size_t n,
+                    std::vector<rt_context*>& out) {
     if ((int)g_cache.size() < first + G) g_cache.resize(first + G, nullptr);
     bool need_scene = false;
     for (int g = 0; g < G; g++) {
-        const rt_context* c = g_cache[first + g];
+        rt_context*& c = g_cache[first + g];
+        if (c && c->device != map[first + g]) {  // the logical -> physical map changed
+            rt_context_destroy(c);
+            c = nullptr;
+        }
         need_scene = need_scene || !c || !same_spheres(c->scene, spheres, n);
     }
     SceneData sd;
@@ -804,7 +890,7 @@ int cached_contexts(int first, int G, const rt_sphere* spheres, size_t n, std::v
     auto work = [&](int g) {
         rt_context*& c = g_cache[first + g];
         int rc = RT_OK;
-        if (!c) rc = rt_context_create(first + g, &c);
+        if (!c) rc = rt_context_create(map[first + g], &c);
         if (!rc && !same_spheres(c->scene, spheres, n)) rc = upload_scene(c, sd);
         rcs[g] = rc;
         if (rc) msgs[g] = rt_last_error();  // thread-local: carried back to the caller's thread
@@ -847,9 +933,10 @@ int rt_render(const rt_camera* cam, const rt_sphere* spheres, size_t n, const rt
         rt_set_last_error("pixel_stride must be >= 3");
         return RT_ERR_INVALID;
     }
-    int count = 0;
-    HIP_CHECK(hipGetDeviceCount(&count));
-    if (count <= 0) { rt_set_last_error("no HIP device"); return RT_ERR_NO_DEVICE; }
+    std::vector<int> map;
+    rc = device_map(map);
+    if (rc) return rc;
+    const int count = (int)map.size();
     const int first = o.device;
     int G = o.n_gpus > 0 ? o.n_gpus : count - first;
     if (first < 0 || first + G > count || G <= 0) {
@@ -862,7 +949,7 @@ int rt_render(const rt_camera* cam, const rt_sphere* spheres, size_t n, const rt
 
     std::lock_guard<std::mutex> lock(g_cache_mu);
     std::vector<rt_context*> ctxs;
-    rc = cached_contexts(first, G, spheres, n, ctxs);
+    rc = cached_contexts(map, first, G, spheres, n, ctxs);
     if (rc) return rc;
     std::vector<uint32_t> rows(G);
     for (int g = 0; g < G; g++) {
@@ -899,7 +986,8 @@ int rt_render(const rt_camera* cam, const rt_sphere* spheres, size_t n, const rt
         HIP_CHECK(hipSetDevice(c->device));
         HIP_CHECK(hipStreamSynchronize(c->stream));
         if (c->h_stats[2]) {
-            rt_set_last_error("render kernel: a wave timed out waiting for a running-sum hand-off");
+            HIP_CHECK(hipMemset(c->d_ctr + rtk::kErrWord, 0, sizeof(uint64_t)));  // reported: clear the sticky word
+            rt_set_last_error(kStallMsg);
             return RT_ERR_HIP;
         }
         stats[0] += c->h_stats[0];

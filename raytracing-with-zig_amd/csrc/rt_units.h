@@ -29,12 +29,18 @@ __device__ __forceinline__ void st_wt(double* p, double v) {  // global_store_dw
     __hip_atomic_store((gu64*)p, __builtin_bit_cast(unsigned long long, v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// A wave that cannot claim and has nothing to trace sleeps between polls; a bug that broke the
-// dependency chain would otherwise hang the GPU, so each continuous wait is bounded (≈ 0.5 s of
-// sleeping; the count restarts whenever the wave finalises or claims a unit, so a long launch's
-// many short waits never add up to it): past it the wave reports it in ctr[kErrWord] and gives up
-// (the host returns RT_ERR_HIP).
-constexpr uint32_t kSpinLimit = 1u << 22;
+// A wave that cannot claim and has nothing to trace sleeps between polls.  A bug that broke the
+// dependency chain would otherwise hang the GPU, so a wait is bounded — by GLOBAL progress, not by
+// this wave's own: the launch counts its finalised units in ctr[kProgWord], and a waiting wave
+// gives up only when that count has not moved for kStallTicks of wall clock (s_memrealtime, a
+// constant 100 MHz).  A predecessor unit may legitimately take seconds to trace (a huge scene on
+// the linear walk), but while any wave of the launch finalises anything the wait goes on.  Past
+// the bound the wave reports it in the sticky ctr[kErrWord] and gives up (the host returns
+// RT_ERR_HIP).  The timer restarts whenever this wave claims or finalises a unit.  The clock is kept
+// as its low 32 bits (wrapping differences are exact below 2^32 ticks = 42.9 s); a 64-bit timer
+// cost 12 VGPRs of the path loop through SGPR spills.
+constexpr uint32_t kStallTicks = 40u * 100000000u;  // 40 s without any unit finalised
+__device__ __forceinline__ uint64_t realtime() { return __builtin_amdgcn_s_memrealtime(); }
 
 
 // Wave-uniform scheduler state (every member is the same in all 64 lanes).  kDirect: direct mode
@@ -49,7 +55,8 @@ struct UnitSched {
     uint32_t cur_tile = 0, cur_s0 = 0;
     uint32_t st_u[kSlots];           // unit id held by each slot
     uint32_t spins = 0;              // sleeps in all (diagnostics)
-    uint32_t wait_run = 0;           // sleeps since the last finalisation or claim
+    uint32_t wait_t0 = 0;            // realtime (low word, | 1) when the current wait last saw global progress (0: not waiting)
+    uint32_t wait_prog = 0;          // ctr[kProgWord] as this wave last read it
     uint32_t seen = 0;               // direct mode: item position after this wave's last claim
     uint32_t waves = 1;              // direct mode: the launch's waves
     uint32_t seg = 0, empty = 0;     // direct mode: segment claimed from; segments found empty
@@ -57,7 +64,7 @@ struct UnitSched {
     uint32_t n_dep_wait = 0;   // diagnostics (instrumented build): finalisations deferred on a flag
     uint32_t n_no_slot = 0;    // ... refills stopped for want of a free slot
     bool drained = false;            // the claim counter is exhausted
-    bool failed = false;             // spin limit reached (reported in ctr[kErrWord])
+    bool failed = false;             // stall bound reached (reported in ctr[kErrWord])
 
     __device__ UnitSched(const UnitArgs& a, uint32_t wave) : ua(a), ring(a.ring + (size_t)wave * kRingWaveDoubles) {
         if constexpr (kDirect) {
@@ -90,7 +97,7 @@ struct UnitSched {
                 if (lane == 0) t = (uint32_t)atomicAdd(ua.ctr + kCtrStride * seg, (unsigned long long)k);
                 t = lo + __builtin_amdgcn_readfirstlane(t);
                 if (t < hi) {
-                    wait_run = 0;
+                    wait_t0 = 0;
                     seen = t + k;
                     cur = t;
                     end = hi - t < k ? hi : t + k;
@@ -124,7 +131,7 @@ struct UnitSched {
         for (uint32_t j = 0; j < kSlots; ++j) st_u[j] = j == js ? u : st_u[j];
         busy |= 1u << js;
         cur_slot = js;
-        wait_run = 0;
+        wait_t0 = 0;
         cur = 0;
         end = n * 64;
         cur_tile = tile;
@@ -213,7 +220,15 @@ struct UnitSched {
                 ++n_dep_wait;
                 continue;
             }
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keeps the sc1 loads below the poll
+            // Ordering of the hand-off, pinned explicitly rather than by agent-scope acquire/release
+            // (which gfx950 implements as buffer_inv sc1 / buffer_wbl2 sc1: an invalidate or a
+            // write-back of the whole L2 per hand-off).  Hardware: the sums loads below are issued
+            // only after the flag's value has returned (readfirstlane + the scalar branch above wait
+            // for it), and they are sc1 loads; the producer drains its sc1 sum stores
+            // (s_waitcnt vmcnt(0)) before its flag store.  Compiler: the fence and the "memory"
+            // clobber keep every load below this point.
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            asm volatile("" ::: "memory");
             uint32_t s0, n;
             chunk_range(ua, k, &s0, &n);
             const uint32_t q = tile * 64 + lane;
@@ -250,10 +265,14 @@ struct UnitSched {
                 }
             }
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains before the flag
-            if (lane == 0 && k + 1 < ua.n_chunks)
-                __hip_atomic_store((gu32*)ua.flags + tile, k + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (lane == 0) {
+                if (k + 1 < ua.n_chunks)
+                    __hip_atomic_store((gu32*)ua.flags + tile, k + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                // global progress for the bounded waits (no return value: the wave does not wait on it)
+                __hip_atomic_fetch_add((gu64*)ua.ctr + kProgWord, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
             busy &= ~(1u << j);
-            wait_run = 0;
+            wait_t0 = 0;
             return true;
         }
         return false;
@@ -262,7 +281,15 @@ struct UnitSched {
     // Nothing to trace in this wave: wait for a dependency (bounded).  False: give up (reported).
     __device__ __forceinline__ bool wait(uint32_t lane) {
         ++spins;
-        if (++wait_run > kSpinLimit) {
+        uint32_t prog = 0;
+        if (lane == 0)
+            prog = (uint32_t)__hip_atomic_load((gu64*)ua.ctr + kProgWord, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        prog = __builtin_amdgcn_readfirstlane(prog);
+        const uint32_t now = (uint32_t)realtime() | 1u;
+        if (wait_t0 == 0 || prog != wait_prog) {
+            wait_t0 = now;
+            wait_prog = prog;
+        } else if (now - wait_t0 > kStallTicks) {
             if (lane == 0) atomicOr(ua.ctr + kErrWord, 1ull);
             failed = true;
             return false;

@@ -83,3 +83,35 @@ def test_assemble_order():
             if r + k * world < H:
                 g[r, k] = r + k * world
     assert rdist.assemble(g, H).flatten().tolist() == list(range(H))
+
+
+def _bench(args, env_extra=None, drop=("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")):
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in drop}
+    env.update(env_extra or {})
+    p = subprocess.run([sys.executable, os.path.join(root, "bench.py")] + args, capture_output=True, text=True,
+                       timeout=240, env=env, cwd=root)
+    lines = [json.loads(x) for x in p.stdout.splitlines() if x.startswith("{")]
+    return p.returncode, lines, p.stderr
+
+
+def test_bench_spawns_ranks_without_launcher():
+    """`bench.py --gpus 2` with no launcher (no WORLD_SIZE) starts the 2 ranks itself and they form
+    one process group (--launch-check: gloo, no rendering), instead of silently running 1 GPU."""
+    rc, lines, err = _bench(["--gpus", "2", "--launch-check"])
+    assert rc == 0, err[-2000:]
+    assert lines == [{"launch_check": True, "n_gpus": 2, "gpus_arg": 2}]
+
+
+def test_bench_refuses_what_it_cannot_run():
+    """Mismatched --gpus vs a launcher's WORLD_SIZE, and nccl ranks without one device each (this
+    container has none), exit non-zero instead of reporting a 1-GPU number."""
+    rc, lines, _ = _bench(["--gpus", "2", "--launch-check"], {"WORLD_SIZE": "3", "RANK": "0", "LOCAL_RANK": "0"},
+                          drop=())
+    assert rc != 0 and lines == []
+    if torch.cuda.device_count() < 2:
+        rc, lines, err = _bench(["--gpus", "2", "--steps", "1", "--warmup", "0"])
+        assert rc != 0 and lines == [] and "need 2 visible GPUs" in err

@@ -51,3 +51,41 @@ def test_8k_image_rows_bit_exact(oracle, mode, monkeypatch):
     r.sync()
     assert torch.equal(part[0], full[1000]) and torch.equal(part[1], full[3999])
     r.close()
+
+
+def test_huge_scene_linear_walk_ring_mode(oracle, monkeypatch):
+    """70 000 spheres: more than the BVH's depth bound holds (2^15 two-sphere leaves), so the tree
+    does not build and the kernel walks the whole list (smem_u4) for every ray — ~100x the final
+    scene's per-segment cost.  Ring mode forced with 2 tiles x 40 spp, so units of the same tile
+    are chained across waves and their hand-off waits span slow predecessor units; the bounded wait
+    (rt_units.h: global progress, not the wave's own) must not give up, and the bits must equal
+    oracle B's linear scan."""
+    from rtzig.abi import D3, RtSphere
+    monkeypatch.setenv("RTZIG_UNIT_MODE", "ring")
+    rng = np.random.default_rng(65537)
+    n = 70_000
+    arr = (RtSphere * n)()
+    arr[0] = RtSphere(center=D3(0, -1000, 0), radius=1000.0, material=0, albedo=D3(0.5, 0.5, 0.5))
+    c = rng.uniform([-40, 0.05, -40], [40, 2.5, 40], (n, 3))
+    rad = rng.uniform(0.02, 0.12, n)
+    mats = rng.integers(0, 3, n)
+    alb = rng.uniform(0, 1, (n, 3))
+    for k in range(1, n):
+        arr[k] = RtSphere(center=D3(*c[k]), radius=float(rad[k]), material=int(mats[k]), albedo=D3(*alb[k]),
+                          fuzz=0.2, refraction_index=1.5)
+    scene = rtzig.Scene.init(99)
+    scene.world = arr
+    cam = (rtzig.Camera.builder(16, 2.0).setScene(scene).setDefocusAngle(0.6).setFocusDist(10.0)
+           .setViewport((13, 2, 3), (0, 0, 0), 20.0).setSamplesPerPixel(40).build())
+    assert cam.width * cam.height == 128
+    r = rtzig.DeviceRenderer(0)
+    r.set_scene(arr)
+    out = torch.zeros((cam.height, cam.width, 3), dtype=torch.float64, device="cuda:0")
+    stats = torch.zeros(2, dtype=torch.int64, device="cuda:0")
+    r.render_rows_async(cam.cam, out.data_ptr(), d_stats_ptr=stats.data_ptr())
+    r.sync()  # raises if a wave gave up waiting
+    assert r.kernel_name() == "smem_u4"  # the list walk: no tree for this many spheres
+    r.close()
+    ref, rays = oracle.render_b(cam.cam, arr, threads=16)
+    assert np.array_equal(out.cpu().numpy(), ref)
+    assert int(stats[0]) == rays

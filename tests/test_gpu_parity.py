@@ -45,18 +45,32 @@ def test_final_scene_golden_config_bit_exact(oracle):
     assert st["rays"] == rays
 
 
-def test_final_scene_statistically_matches_reference_golden(golden_dir):
-    """Parity ladder step 3: GPU (per-sample streams) vs the reference's own chapter14.ppm
-    (sequential stream).  Tolerance per north_star: per-channel image mean |delta| <= 1.0 (8-bit
-    units) and 8x8 box-filtered RMSE <= 2.0."""
+def _box_rmse(a, b):
+    box = lambda x: x[:224].reshape(28, 8, 50, 8, 3).astype(np.float64).mean(axis=(1, 3))
+    return float(np.sqrt(((box(a) - box(b)) ** 2).mean()))
+
+
+def _check_vs_chapter14(oracle, rgb, golden_dir):
+    """SURVEY §8(c) ladder 3: GPU (per-sample streams) vs the reference's own chapter14.ppm
+    (sequential stream), calibrated like configs 2/3: per-channel image-mean |delta| <= 1.0 (8-bit
+    units) and 8x8 box RMSE <= 1.5x the A-vs-B RMSE.  Oracle A reproduces chapter14.ppm byte for
+    byte (test_oracle.py), so the A side of the floor is the fixture itself; the B side is oracle B
+    on the oracle's own scene and camera (golden_params)."""
     from oracle_lib import read_ppm
+    _, _, gold = read_ppm(open(os.path.join(golden_dir, "chapter14.ppm"), "rb").read())
+    spheres, _ = oracle.scene_final(0xDEADBEEF)
+    b, _ = oracle.render_b(oracle.camera_build(golden_params()), spheres, threads=16)
+    floor = _box_rmse(gold, oracle.to_rgb8(b))
+    assert np.abs(rgb.astype(np.float64).mean(axis=(0, 1)) - gold.astype(np.float64).mean(axis=(0, 1))).max() <= 1.0
+    assert _box_rmse(rgb, gold) <= 1.5 * floor, (_box_rmse(rgb, gold), floor)
+
+
+def test_final_scene_statistically_matches_reference_golden(oracle, golden_dir):
+    """The bench scene at the golden test's configuration (main.zig:41-55) vs chapter14.ppm, with
+    the calibrated A-vs-B rule of _check_vs_chapter14."""
     cam = rtzig.final_scene_camera(width=400, aspect_ratio=16 / 9, spp=10)
     rgb, _ = gpu_render(cam, cam.scene.world, n_gpus=1, output="rgb8")
-    _, _, gold = read_ppm(open(os.path.join(golden_dir, "chapter14.ppm"), "rb").read())
-    a, b = rgb.astype(np.float64), gold.astype(np.float64)
-    assert np.abs(a.mean(axis=(0, 1)) - b.mean(axis=(0, 1))).max() <= 1.0
-    box = lambda x: x[:224].reshape(28, 8, 50, 8, 3).mean(axis=(1, 3))
-    assert np.sqrt(((box(a) - box(b)) ** 2).mean()) <= 2.0
+    _check_vs_chapter14(oracle, rgb, golden_dir)
 
 
 def test_chapter13_crop_bit_exact(oracle):
@@ -76,11 +90,11 @@ def test_final_1200x800_rows_bit_exact(oracle):
 
 
 def test_rgb8_output_matches_to_rgb(oracle):
-    """Fused Color.toRgb epilogue == host toRgb of the linear output (color.zig:63-80)."""
+    """Fused Color.toRgb epilogue (color.zig:63-80) == oracle B's image through the oracle's toRgb."""
     cam = rtzig.final_scene_camera(width=400, aspect_ratio=16 / 9, spp=3)
-    lin, _ = gpu_render(cam, cam.scene.world, n_gpus=1)
     rgb, _ = gpu_render(cam, cam.scene.world, n_gpus=1, output="rgb8")
-    assert np.array_equal(rgb, oracle.to_rgb8(lin))
+    ref, _ = oracle.render_b(cam.cam, cam.scene.world, threads=16)
+    assert np.array_equal(rgb, oracle.to_rgb8(ref))
 
 
 def test_row_partition_invariance():
@@ -172,22 +186,57 @@ def test_large_scene_global_memory_variant(oracle):
     assert np.array_equal(out, ref) and st["rays"] == rays
 
 
-def test_multi_gpu_call_equals_single(oracle):
-    """rt_render over every visible device == one device (row interleave + host un-interleave)."""
+@pytest.mark.parametrize("device_map", ["0,0", "0,0,0", "0,0,0,0,0,0,0,0", None])
+def test_multi_gpu_call_equals_single(oracle, device_map, monkeypatch):
+    """rt_render over several devices (n_gpus=0: all of them) == oracle B, bit for bit: its multi-
+    device branch (contexts created on host threads, one stream each, row j on device j mod G,
+    host un-interleave, stats summed) with G = 2, 3 and 8 logical devices mapped onto GPU 0
+    (RTZIG_DEVICE_MAP, rt_runtime.cpp), and over the real devices when there are several.  f64 with
+    the Zig shim's stride 4, and the fused RGB8 output."""
     import torch
-    if torch.cuda.device_count() < 2:
-        pytest.skip("needs more than one visible GPU (tests/test_gpu_multirank.py covers the rank path)")
+    if device_map is None:
+        if torch.cuda.device_count() < 2:
+            pytest.skip("one visible GPU: the mapped cases cover the multi-device branch")
+        monkeypatch.delenv("RTZIG_DEVICE_MAP", raising=False)
+        G = torch.cuda.device_count()
+    else:
+        monkeypatch.setenv("RTZIG_DEVICE_MAP", device_map)
+        G = len(device_map.split(","))
+    lib = rtzig.load()
     cam = rtzig.final_scene_camera(width=200, aspect_ratio=16 / 9, spp=4)
-    one, _ = gpu_render(cam, cam.scene.world, n_gpus=1)
-    many, _ = gpu_render(cam, cam.scene.world, n_gpus=0)
-    assert np.array_equal(one, many)
+    ref, rays = oracle.render_b(cam.cam, cam.scene.world, threads=16)
+    out = np.full((cam.height, cam.width, 4), -7.0)
+    st = (C.c_uint64 * 2)()
+    opts = rtzig.RtOptions(n_gpus=0, pixel_stride=4, output_format=0, stats_out=C.cast(st, C.POINTER(C.c_uint64)))
+    rc = lib.rt_render(C.byref(cam.cam), cam.scene.world, len(cam.scene.world), C.byref(opts),
+                       out.ctypes.data_as(C.c_void_p))
+    assert rc == 0, lib.rt_last_error()
+    assert np.array_equal(out[..., :3], ref) and (out[..., 3] == -7.0).all()
+    assert st[0] == rays and st[1] == cam.width * cam.height * 4
+    rgb, _ = gpu_render(cam, cam.scene.world, n_gpus=0, output="rgb8")
+    assert np.array_equal(rgb, oracle.to_rgb8(ref))
+    if device_map is not None:  # the logical device count is what the map says
+        with pytest.raises(rtzig.lib.RtError):
+            gpu_render(cam, cam.scene.world, n_gpus=G + 1)
 
 
-def test_pixel_stride_4_matches_zig_vector_layout():
-    """Zig's @Vector(3, f64) is 32 bytes: the shim passes pixel_stride=4."""
+def test_multi_device_ring_mode_bit_exact(oracle, monkeypatch):
+    """The multi-device branch with every context in ring mode (in-kernel ordered accumulation and
+    its cross-wave hand-off; three 1.2 GB workspaces on GPU 0)."""
+    monkeypatch.setenv("RTZIG_DEVICE_MAP", "0,0,0")
+    monkeypatch.setenv("RTZIG_UNIT_MODE", "ring")
+    cam = rtzig.final_scene_camera(width=160, aspect_ratio=1.5, spp=60)
+    out, st = gpu_render(cam, cam.scene.world, n_gpus=0)
+    ref, rays = oracle.render_b(cam.cam, cam.scene.world, threads=16)
+    assert np.array_equal(out, ref) and st["rays"] == rays
+    rtzig.release_cached_contexts()
+
+
+def test_pixel_stride_4_matches_zig_vector_layout(oracle):
+    """Zig's @Vector(3, f64) is 32 bytes: the shim passes pixel_stride=4 (compared with oracle B)."""
     lib = rtzig.load()
     cam = rtzig.final_scene_camera(width=64, aspect_ratio=16 / 9, spp=2)
-    ref, _ = gpu_render(cam, cam.scene.world, n_gpus=1)
+    ref, _ = oracle.render_b(cam.cam, cam.scene.world, threads=16)
     out = np.full((cam.height, cam.width, 4), -7.0)
     opts = rtzig.RtOptions(n_gpus=1, pixel_stride=4, output_format=0)
     rc = lib.rt_render(C.byref(cam.cam), cam.scene.world, len(cam.scene.world), C.byref(opts),
@@ -206,16 +255,29 @@ def test_camera_render_api(tmp_path, golden_dir):
     assert len(data) == 270016 and data.startswith(b"P6\n400 225\n255\n") and data.endswith(b"\n")
 
 
-def test_c_harness_end_to_end(tmp_path):
-    """tools/rt_render_c.c drives the ABI exactly like the Zig shim: its P6 file
-    equals the Python path's fused-RGB8 render of the same preset."""
+@pytest.mark.parametrize("device_map", ["0,0,0", "0", None])
+def test_c_harness_end_to_end(oracle, golden_dir, tmp_path, device_map):
+    """The drop-in exactly as the Zig shim calls it (reference main.zig:41-55 ->
+    camera.zig:123-145 -> saveBinary): tools/rt_render_c.c builds the golden configuration (400x225,
+    10 spp, seed 0xdeadbeef, 485 spheres) through the ABI and calls rt_render with the shim's
+    n_gpus = 0 — with RTZIG_DEVICE_MAP=0,0,0 that is the multi-device branch over three contexts.
+    Its P6 file must equal oracle B's P6 byte for byte, and match the reference's chapter14.ppm
+    under the calibrated statistical rule."""
     import subprocess
+    from oracle_lib import read_ppm
     exe = os.path.join(os.path.dirname(rtzig.LIB_PATH), "rt_render_c")
     out = str(tmp_path / "chapter14.ppm")
-    subprocess.run([exe, out, "400", "10", "0xdeadbeef"], check=True, capture_output=True, timeout=300)
+    env = dict(os.environ)
+    env.pop("RTZIG_DEVICE_MAP", None)
+    if device_map is not None:
+        env["RTZIG_DEVICE_MAP"] = device_map
+    subprocess.run([exe, out, "400", "10", "0xdeadbeef"], check=True, capture_output=True, timeout=300, env=env)
     cam = rtzig.final_scene_camera(width=400, aspect_ratio=16 / 9, spp=10)
-    rgb, _ = gpu_render(cam, cam.scene.world, output="rgb8")
-    assert open(out, "rb").read() == rtzig.encode_p6(rgb, 400, 225)
+    ref, _ = oracle.render_b(cam.cam, cam.scene.world, threads=16)
+    data = open(out, "rb").read()
+    assert data == oracle.ppm_p6(oracle.to_rgb8(ref), 400, 225)
+    _, _, rgb = read_ppm(data)
+    _check_vs_chapter14(oracle, rgb, golden_dir)
 
 
 @pytest.mark.parametrize("mode", ["ring", "direct"])
