@@ -146,7 +146,20 @@ struct KernelParams {
 // on 32 different banks of the 64 (gcd(26, 64) = 2), so per-lane random ds_read_b64 gathers
 // spread over the whole bank row.  Leaves (2 slots: 80 B = 5 x 16, read as ds_read_b128) start
 // at the next 16-B boundary after the nodes.
-constexpr int kBlockBvh = 512;     // 8 waves; 2 blocks per CU share the LDS budget
+#ifndef RTZIG_BVH_BLOCK
+#define RTZIG_BVH_BLOCK 512
+#endif
+#ifndef RTZIG_STACK16
+#define RTZIG_STACK16 0
+#endif
+constexpr int kBlockBvh = RTZIG_BVH_BLOCK;  // 8 waves; 2 blocks per CU share the LDS budget (build knob)
+// per-lane stack entry of the BVH walk (build knob: int16 holds every ref of a tree whose nodes and
+// leaves each span < 32 KiB, rt_kernel.hip StackOps)
+#if RTZIG_STACK16
+typedef int16_t StackEntry;
+#else
+typedef int32_t StackEntry;
+#endif
 constexpr size_t kLdsSceneBudget = 80 * 1024;  // tree + stacks of one block (2 blocks per CU's 160 KiB)
 constexpr int kMaxDepthBvh = 16;   // == rtbvh::kMaxDepth: bound on per-lane LDS stack entries (entry 0: "done")
 #ifndef RTZIG_LEAF
@@ -179,7 +192,7 @@ struct BvhArgs {
     float origin_bound;
     uint32_t pad;
 };
-// LDS layout of the BVH kernel: [nodes, padded to 16 B][leaves][stacks: stack_depth x kBlockBvh x 4 B]
+// LDS layout of the BVH kernel: [nodes, padded to 16 B][leaves][stacks: stack_depth x kBlockBvh x sizeof(StackEntry)]
 __host__ __device__ inline uint32_t bvh_leaves_offset(uint32_t n_nodes) {
     return (n_nodes * (uint32_t)sizeof(BvhNode) + 15u) & ~15u;
 }

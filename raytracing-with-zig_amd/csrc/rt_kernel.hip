@@ -32,6 +32,7 @@
 #include <climits>
 #include <cstring>
 #include <mutex>
+#include <type_traits>
 #include <vector>
 
 #include "rt_device.h"
@@ -113,6 +114,106 @@ __device__ __forceinline__ void camera_finish(double px, double py, Ray& r) {
     const v3 ddv = mk(dw2d(B[6], B[7]), dw2d(B[8], B[9]), dw2d(B[10], B[11]));
     const v3 origin = (center + muls(ddu, px)) + muls(ddv, py);
     r.dir = r.dir - origin;
+    r.orig = origin;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Fast mode (RT_PRECISION_F32, statistical parity only; DESIGN.md "Fast mode"): the same path loop,
+// walk and scheduler instantiated with kF32 = true, shading, sampling and leaf tests in f32 with
+// single-instruction v_rcp_f32 / v_rsq_f32 / v_sqrt_f32 and FMA allowed (the pragma in each helper).
+// A uniform is 24 bits of the same per-(pixel, sample) Xoshiro256++ stream; paired draws take both
+// 32-bit halves of one word.
+// ------------------------------------------------------------------------------------------------
+namespace fm {
+struct f3 {
+    float x, y, z;
+};
+__device__ __forceinline__ f3 mk(float x, float y, float z) { return f3{x, y, z}; }
+__device__ __forceinline__ f3 add(f3 a, f3 b) { return f3{a.x + b.x, a.y + b.y, a.z + b.z}; }
+__device__ __forceinline__ f3 sub(f3 a, f3 b) { return f3{a.x - b.x, a.y - b.y, a.z - b.z}; }
+__device__ __forceinline__ f3 mul(f3 a, f3 b) { return f3{a.x * b.x, a.y * b.y, a.z * b.z}; }
+__device__ __forceinline__ f3 neg(f3 a) { return f3{-a.x, -a.y, -a.z}; }
+__device__ __forceinline__ f3 muls(f3 a, float s) { return f3{a.x * s, a.y * s, a.z * s}; }
+__device__ __forceinline__ float dot(f3 a, f3 b) {
+#pragma clang fp contract(fast)
+    return a.x * b.x + a.y * b.y + a.z * b.z;
+}
+__device__ __forceinline__ float len_sq(f3 a) { return dot(a, a); }
+__device__ __forceinline__ f3 unit(f3 a) { return muls(a, __builtin_amdgcn_rsqf(len_sq(a))); }
+__device__ __forceinline__ f3 reflect(f3 v, f3 n) { return sub(v, muls(n, 2.0f * dot(v, n))); }
+__device__ __forceinline__ f3 refract(f3 v, f3 n, float eta) {
+#pragma clang fp contract(fast)
+    const float cos_t = __builtin_fminf(-dot(v, n), 1.0f);
+    const f3 r_perp = muls(add(v, muls(n, cos_t)), eta);
+    return sub(r_perp, muls(n, __builtin_sqrtf(__builtin_fabsf(1.0f - len_sq(r_perp)))));
+}
+__device__ __forceinline__ bool near_zero(f3 v) { return v.x < 1e-8f && v.y < 1e-8f && v.z < 1e-8f; }  // vec.zig:26-29
+__device__ __forceinline__ v3 to64(f3 a) { return v3{a.x, a.y, a.z}; }
+// U[0, 1) from the top 24 bits of one Xoshiro256++ word (exact in f32); uniform2 takes two from one
+// word (the top 24 bits of each 32-bit half), halving the generator work of paired draws
+__device__ __forceinline__ float uniform(Rng& g) { return (float)(uint32_t)(g.next() >> 40) * 0x1p-24f; }
+__device__ __forceinline__ void uniform2(Rng& g, float& a, float& b) {
+    const uint64_t w = g.next();
+    a = (float)(uint32_t)(w >> 40) * 0x1p-24f;
+    b = (float)((uint32_t)w >> 8) * 0x1p-24f;
+}
+__device__ __forceinline__ float pm1(float u) { return __builtin_fmaf(2.0f, u, -1.0f); }
+struct Ray {
+    f3 orig, dir;
+};
+}  // namespace fm
+
+// getRay (camera.zig:187-215) in f32 from KernelParams::fcam (kernarg scalar loads at use, like the
+// f64 form below); the defocus disk sample is drawn by the trip loop as in parity mode
+constexpr int kFcam = (int)offsetof(KernelParams, fcam);
+static_assert(kFcam % 4 == 0, "fcam kernarg offset");
+__device__ __forceinline__ float fw(uint32_t w) { return __builtin_bit_cast(float, w); }
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ bool camera_start(uint32_t i, uint32_t j, Rng& g, fm::Ray& r) {
+#pragma clang fp contract(fast)
+    u32x16 A;  // fcam[0..15]
+    u32x4 B;   // fcam[16..19]
+    const uint64_t kp = (uint64_t)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile(
+        "s_load_dwordx16 %0, %2, %3\n\t"
+        "s_load_dwordx4 %1, %2, %4\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=s"(A), "=s"(B)
+        : "s"(kp), "i"(kFcam), "i"(kFcam + 64));
+    const fm::f3 center = fm::mk(fw(A[0]), fw(A[1]), fw(A[2]));
+    const fm::f3 p0 = fm::mk(fw(A[3]), fw(A[4]), fw(A[5]));
+    const fm::f3 du = fm::mk(fw(A[6]), fw(A[7]), fw(A[8]));
+    const fm::f3 dv = fm::mk(fw(A[9]), fw(A[10]), fw(A[11]));
+    const float defocus_angle = fw(B[2]);
+    float ox, oy;
+    fm::uniform2(g, ox, oy);
+    ox -= 0.5f;
+    oy -= 0.5f;
+    const fm::f3 ps = fm::add(fm::add(p0, fm::muls(du, (float)i + ox)), fm::muls(dv, (float)j + oy));
+    r.orig = center;
+    if (defocus_angle <= 0) {
+        r.dir = fm::sub(ps, center);
+        return false;
+    }
+    r.dir = ps;
+    return true;
+}
+__device__ __forceinline__ void camera_finish(float px, float py, fm::Ray& r) {
+#pragma clang fp contract(fast)
+    u32x16 A;
+    u32x4 B;
+    const uint64_t kp = (uint64_t)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile(
+        "s_load_dwordx16 %0, %2, %3\n\t"
+        "s_load_dwordx4 %1, %2, %4\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=s"(A), "=s"(B)
+        : "s"(kp), "i"(kFcam), "i"(kFcam + 64));
+    const fm::f3 center = fm::mk(fw(A[0]), fw(A[1]), fw(A[2]));
+    const fm::f3 ddu = fm::mk(fw(A[12]), fw(A[13]), fw(A[14]));
+    const fm::f3 ddv = fm::mk(fw(A[15]), fw(B[0]), fw(B[1]));
+    const fm::f3 origin = fm::add(fm::add(center, fm::muls(ddu, px)), fm::muls(ddv, py));
+    r.dir = fm::sub(r.dir, origin);
     r.orig = origin;
 }
 
@@ -323,14 +424,36 @@ struct LeafFilter {
     }
 };
 
-template <bool kLdsNodes>
+// Stack entries are StackT (int32; int16 holds every ref of a tree that fits the LDS: byte offsets
+// < 2^15) strided by kStride (the block size: element i of a lane at stack[i * kStride]); the
+// product kernel uses <int32_t, kBlockBvh>, tools/walk_occupancy.hip other combinations.
+template <class StackT>
+struct StackOps;
+template <>
+struct StackOps<int32_t> {
+    static constexpr int32_t kEnd = kDone;
+    __device__ __forceinline__ static void read(int32_t& v, const int32_t* p) { lds_b32(v, lds_addr(p), 0); }
+};
+template <>
+struct StackOps<int16_t> {
+    static constexpr int32_t kEnd = INT16_MIN;  // sign-extended by ds_read_i16
+    __device__ __forceinline__ static void read(int32_t& v, const int16_t* p) {
+        asm volatile("ds_read_i16 %0, %1" : "=v"(v) : "v"(lds_addr(p)));
+    }
+};
+
+template <bool kLdsNodes, int kStride = kBlockBvh, class StackT = int32_t, bool kF32 = false>
 struct BvhWalker {
+    static constexpr int32_t kEnd = StackOps<StackT>::kEnd;  // "walk finished" (stack entry 0)
+    static constexpr bool kFast = kF32;  // fast mode: f32 ray, f32 leaf tests (huge spheres in f64)
+    using RayT = std::conditional_t<kF32, fm::Ray, Ray>;
+    using Real = std::conditional_t<kF32, float, double>;
     const BvhNode* __restrict__ nodes;
     const BvhLeaf* __restrict__ leaves;
     const GeoRec* __restrict__ ageo;     // always-list geometry
     const uint32_t* __restrict__ asid;   // always-list original indices
     uint32_t n_always;
-    int32_t* stack;                      // LDS, element i of this lane at stack[i * kBlockBvh]
+    StackT* stack;                       // LDS, element i of this lane at stack[i * kStride]
     float origin_bound;                  // BvhArgs::origin_bound
     const GeoRec* __restrict__ geo_all;  // the whole list in original order (far-origin lanes)
     uint32_t n_pad;
@@ -414,19 +537,235 @@ struct BvhWalker {
     static constexpr bool kCanSuspend = true;
     struct State {  // a suspended walk (dynamic fetch)
         int32_t cur;
-        int32_t* top;
-        double closest;
+        StackT* top;
+        Real closest;
         uint32_t best;
         bool found;
     };
+    // fast mode's always-list: big spheres (radius < 100 near the origin) in f32, huge ones (the
+    // final scene's r = 1000 ground) in f64 — in f32 a point on a radius-1000 sphere is known only to
+    // ~6e-5 along its normal, so rays leaving it would re-hit it at grazing angles
+    __device__ __forceinline__ void always_f32(const fm::Ray& r, float t_min, float t_max, float& closest, uint32_t& best,
+                                               bool& found) const {
+#pragma clang fp contract(fast)
+        const double ox = r.orig.x, oy = r.orig.y, oz = r.orig.z;
+        const double dx = r.dir.x, dy = r.dir.y, dz = r.dir.z;
+        const double a = (dx * dx + dy * dy) + dz * dz;
+        const float fa = fm::len_sq(r.dir);
+        double cl = (double)t_max;
+        for (uint32_t q = 0; q < n_always; ++q) {
+            const GeoRec s = ageo[q];
+            if (s.r2 < 1e4 && __builtin_fabs(s.cx) + __builtin_fabs(s.cy) + __builtin_fabs(s.cz) < 1e4) {
+                const float fx = (float)s.cx - r.orig.x, fy = (float)s.cy - r.orig.y, fz = (float)s.cz - r.orig.z;
+                const float h = r.dir.x * fx + r.dir.y * fy + r.dir.z * fz;
+                const float c = (fx * fx + fy * fy + fz * fz) - (float)s.r2;
+                const float disc = h * h - fa * c;
+                if (disc >= 0) {
+                    const float sq = __builtin_sqrtf(disc), ia = __builtin_amdgcn_rcpf(fa);
+                    float ts = (h - sq) * ia;
+                    if (!(t_min < ts)) ts = (h + sq) * ia;
+                    if (t_min < ts && (double)ts < cl) {
+                        cl = ts;
+                        best = asid[q];
+                        found = true;
+                    }
+                }
+                continue;
+            }
+            const double cx = s.cx - ox, cy = s.cy - oy, cz = s.cz - oz;
+            const double h = (dx * cx + dy * cy) + dz * cz;
+            const double c = ((cx * cx + cy * cy) + cz * cz) - s.r2;
+            const double disc = h * h - a * c;
+            if (disc >= 0) {
+                const double sq = __builtin_sqrt(disc);
+                double ts = (h - sq) / a;
+                if (!(t_min < ts)) ts = (h + sq) / a;
+                if (t_min < ts && ts < cl) {
+                    cl = ts;
+                    best = asid[q];
+                    found = true;
+                }
+            }
+        }
+        closest = found ? (float)cl : t_max;
+    }
+    // fast mode's leaf: kLeafBvh f32 quadratics with the reciprocal of a
+    __device__ __forceinline__ void leaf_f32(const BvhLeaf* lf, const fm::Ray& r, float t_min, float inv_a, float a,
+                                             float& closest, uint32_t& best, bool& found) const {
+#pragma clang fp contract(fast)
+#pragma unroll
+        for (int u = 0; u < kLeafBvh; ++u) {
+            const LeafGeo s = lf->g[u];
+            const float cx = (float)s.cx - r.orig.x, cy = (float)s.cy - r.orig.y, cz = (float)s.cz - r.orig.z;
+            const float h = r.dir.x * cx + r.dir.y * cy + r.dir.z * cz;
+            const float c = (cx * cx + cy * cy + cz * cz) - (float)s.r2;
+            const float disc = h * h - a * c;
+            if (disc >= 0) {
+                const float sq = __builtin_sqrtf(disc);
+                float ts = (h - sq) * inv_a;
+                if (!(t_min < ts)) ts = (h + sq) * inv_a;
+                if (t_min < ts && ts < closest) {
+                    closest = ts;
+                    best = lf->sid[u];
+                    found = true;
+                }
+            }
+        }
+    }
+
     template <class PR>
-    __device__ __forceinline__ int operator()(const Ray& r, double t_min, double t_max, double* t_hit, PR& pr) const {
+    __device__ __forceinline__ int operator()(const RayT& r, Real t_min, Real t_max, Real* t_hit, PR& pr) const {
         State s;
         return run<false>(r, t_min, t_max, t_hit, pr, s, false);
     }
     template <bool kSusp, class PR>
-    __device__ __forceinline__ int run(const Ray& r, double t_min, double t_max, double* t_hit, PR& pr, State& st,
+    __device__ __forceinline__ int run(const RayT& r, Real t_min, Real t_max, Real* t_hit, PR& pr, State& st,
                                        const bool resume) const {
+        if constexpr (kF32) {
+            return run_f32<kSusp>(r, t_min, t_max, t_hit, pr, st, resume);
+        } else {
+            return run_f64<kSusp>(r, t_min, t_max, t_hit, pr, st, resume);
+        }
+    }
+
+    // The traversal shared by both precisions: lanes advance through internal nodes until each holds a
+    // leaf or is done (cur, top: the lane's walk state; lower / upper: its f32 [t_min, closest]).
+    template <class PR>
+    __device__ __forceinline__ void descend(int32_t& cur, StackT*& top, uint32_t ax, uint32_t ay, uint32_t az,
+                                            f2 inv_x, f2 inv_y, f2 inv_z, f2 noi_x, f2 noi_y, f2 noi_z, float lower,
+                                            float upper, PR& pr) const {
+        while (cur >= 0) {
+            pr.visit();
+            pr.inner_iter();
+            f2 bx0, by0, bz0, bx1, by1, bz1;
+            int32_t ref0, ref1, popped;
+            if constexpr (kLdsNodes) {
+                // nodes start at LDS address 0: the ref is the address.  Seven ds_read_b64
+                // (2 LDS cycles each); left to itself the compiler pairs them into
+                // ds_read2_b64 (8 cycles for the same 16 B) behind extra base adds.
+                const uint32_t a = (uint32_t)cur;
+                i2 refs;
+                lds_b64(bx0, a + ax, 0); lds_b64(bx1, a + ax, 48);
+                lds_b64(by0, a + ay, 0); lds_b64(by1, a + ay, 48);
+                lds_b64(bz0, a + az, 0); lds_b64(bz1, a + az, 48);
+                lds_b64(refs, a, 96);
+                StackOps<StackT>::read(popped, top);
+                asm volatile("s_waitcnt lgkmcnt(0)"
+                             : "+v"(bx0), "+v"(bx1), "+v"(by0), "+v"(by1), "+v"(bz0), "+v"(bz1), "+v"(refs),
+                               "+v"(popped));
+                ref0 = refs.x;
+                ref1 = refs.y;
+            } else {
+                const char* nb = (const char*)nodes + cur;  // byte-offset ref
+                bx0 = *(const f2*)(nb + ax); by0 = *(const f2*)(nb + ay); bz0 = *(const f2*)(nb + az);
+                bx1 = *(const f2*)(nb + 48 + ax); by1 = *(const f2*)(nb + 48 + ay); bz1 = *(const f2*)(nb + 48 + az);
+                ref0 = *(const int32_t*)(nb + 96);
+                ref1 = *(const int32_t*)(nb + 100);
+                popped = *top;
+            }
+            const f2 tx0 = pk_fma_lo(bx0, inv_x, noi_x);
+            const f2 ty0 = pk_fma_lo(by0, inv_y, noi_y);
+            const f2 tz0 = pk_fma_lo(bz0, inv_z, noi_z);
+            const f2 tx1 = pk_fma_lo(bx1, inv_x, noi_x);
+            const f2 ty1 = pk_fma_lo(by1, inv_y, noi_y);
+            const f2 tz1 = pk_fma_lo(bz1, inv_z, noi_z);
+            const float n0 = slab_near(tx0.x, ty0.x, tz0.x, lower), f0 = slab_far(tx0.y, ty0.y, tz0.y, upper);
+            const float n1 = slab_near(tx1.x, ty1.x, tz1.x, lower), f1 = slab_far(tx1.y, ty1.y, tz1.y, upper);
+            // both hit: descend into the nearer child and push the farther one (the store
+            // always happens; it only counts when sp advances); one hit: descend; none: pop.
+            // The three compares are taken as wave masks and combined on the scalar unit, and
+            // the selects are v_cndmask on those masks: 3 compares + 5 selects (the compiler's
+            // form of the same logic re-compared a negated mask on the VALU).
+            const uint64_t m0 = __ballot(n0 <= f0), m1 = __ballot(n1 <= f1), mf = __ballot(n0 <= n1);
+            const uint64_t pick0 = m0 & (~m1 | mf);  // both: nearer; one: that one
+            const uint64_t any = m0 | m1, both = m0 & m1;
+            const int32_t near = sel_mask(ref1, ref0, pick0), far = sel_mask(ref0, ref1, pick0);
+            top[kStride] = (StackT)far;
+            cur = sel_mask(popped, near, any);
+            top += sel_mask(sel_mask(-kStride, 0, any), kStride, both);
+        }
+    }
+
+    template <bool kSusp, class PR>
+    __device__ __forceinline__ int run_f32(const fm::Ray& r, float t_min, float t_max, float* t_hit, PR& pr, State& st,
+                                           const bool resume) const {
+        const float a = fm::len_sq(r.dir);
+        const float inv_a = __builtin_amdgcn_rcpf(a);
+        float closest = t_max;
+        uint32_t best = 0;
+        bool found = false;
+        if (kSusp && resume) {
+            closest = st.closest;
+            best = st.best;
+            found = st.found;
+        } else {
+            always_f32(r, t_min, t_max, closest, best, found);
+            pr.tests(n_always);
+        }
+        const float ox = r.orig.x, oy = r.orig.y, oz = r.orig.z;
+        const float ix = __builtin_amdgcn_fmed3f(__builtin_amdgcn_rcpf(r.dir.x), -1e30f, 1e30f);
+        const float iy = __builtin_amdgcn_fmed3f(__builtin_amdgcn_rcpf(r.dir.y), -1e30f, 1e30f);
+        const float iz = __builtin_amdgcn_fmed3f(__builtin_amdgcn_rcpf(r.dir.z), -1e30f, 1e30f);
+        const uint32_t ax = ix < 0 ? 8u : 0u, ay = 16u + (iy < 0 ? 8u : 0u), az = 32u + (iz < 0 ? 8u : 0u);
+        // origins beyond the boxes' origin bound walk the whole list (exact f64 scan, as in parity mode)
+        const bool far = !(kSusp && resume) &&
+                         __builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(ox), __builtin_fabsf(oy)), __builtin_fabsf(oz)) >
+                             origin_bound;
+        if (__builtin_expect(__ballot(far) != 0, 0)) {
+            if (far) {
+                double t;
+                const Ray r64{fm::to64(r.orig), fm::to64(r.dir)};
+                const int k = world_hit<1>(geo_all, n_pad, r64, (double)t_min, (double)t_max, &t);
+                pr.tests(n_pad);
+                found = k >= 0;
+                best = found ? (uint32_t)k : 0u;
+                closest = (float)t;
+            }
+        }
+        f2 inv_x, inv_y, inv_z, noi_x, noi_y, noi_z;
+        inv_x.x = ix; inv_y.x = iy; inv_z.x = iz;
+        noi_x.x = -(ox * ix); noi_y.x = -(oy * iy); noi_z.x = -(oz * iz);
+        float lower = t_min;
+        lower = lower - __builtin_fabsf(lower) * 0x1p-20f - 1e-30f;
+        float upper = closest + __builtin_fabsf(closest) * 0x1p-20f;
+        StackT* top = stack;
+        int32_t cur = far ? kEnd : 0;
+        if (kSusp && resume) {
+            top = st.top;
+            cur = st.cur;
+        }
+        while (cur != kEnd) {
+            descend(cur, top, ax, ay, az, inv_x, inv_y, inv_z, noi_x, noi_y, noi_z, lower, upper, pr);
+            if (cur != kEnd) {
+                pr.leaf_iter();
+                leaf_f32((const BvhLeaf*)((const char*)leaves + (uint32_t)(~cur)), r, t_min, inv_a, a, closest, best, found);
+                pr.tests(kLeafBvh);
+                upper = closest + __builtin_fabsf(closest) * 0x1p-20f;
+                cur = *top;
+                top -= kStride;
+            }
+            if constexpr (kSusp) {
+                const uint64_t walking = __ballot(cur != kEnd);
+                if (walking != 0 && 64 - __popcll(walking) >= kRefetchK) break;
+            }
+        }
+        if constexpr (kSusp) {
+            if (cur != kEnd) {
+                st.cur = cur;
+                st.top = top;
+                st.closest = closest;
+                st.best = best;
+                st.found = found;
+                return kSuspended;
+            }
+        }
+        *t_hit = closest;
+        return found ? (int)best : -1;
+    }
+
+    template <bool kSusp, class PR>
+    __device__ __forceinline__ int run_f64(const Ray& r, double t_min, double t_max, double* t_hit, PR& pr, State& st,
+                                           const bool resume) const {
         const double a = len_sq(r.dir);
         double closest = t_max;
         uint32_t best = 0;
@@ -505,10 +844,10 @@ struct BvhWalker {
         float upper = (float)closest;
         upper = upper + __builtin_fabsf(upper) * 0x1p-20f;
 
-        // stack: entry 0 holds kDone (written once per lane at kernel start), entries 1..sp the
-        // pushed far children; a pop reads entry sp, so popping the empty stack yields kDone
-        int32_t* top = stack;  // this lane's stack entry sp (entry i at stack[i * kBlockBvh])
-        int32_t cur = far ? kDone : 0;  // root
+        // stack: entry 0 holds kEnd (written once per lane at kernel start), entries 1..sp the
+        // pushed far children; a pop reads entry sp, so popping the empty stack yields kEnd
+        StackT* top = stack;  // this lane's stack entry sp (entry i at stack[i * kStride])
+        int32_t cur = far ? kEnd : 0;  // root
         if constexpr (kSusp) {
             if (resume) {
                 top = st.top;
@@ -518,58 +857,9 @@ struct BvhWalker {
         // while-while (Aila & Laine 2009): every lane advances through internal nodes until it
         // holds a leaf (or is done); then the lanes with a leaf test its spheres together, so the
         // f64 leaf work runs with most lanes active instead of whenever any one lane hits a leaf.
-        while (cur != kDone) {
-            while (cur >= 0) {
-                pr.visit();
-                pr.inner_iter();
-                f2 bx0, by0, bz0, bx1, by1, bz1;
-                int32_t ref0, ref1, popped;
-                if constexpr (kLdsNodes) {
-                    // nodes start at LDS address 0: the ref is the address.  Seven ds_read_b64
-                    // (2 LDS cycles each); left to itself the compiler pairs them into
-                    // ds_read2_b64 (8 cycles for the same 16 B) behind extra base adds.
-                    const uint32_t a = (uint32_t)cur;
-                    i2 refs;
-                    lds_b64(bx0, a + ax, 0); lds_b64(bx1, a + ax, 48);
-                    lds_b64(by0, a + ay, 0); lds_b64(by1, a + ay, 48);
-                    lds_b64(bz0, a + az, 0); lds_b64(bz1, a + az, 48);
-                    lds_b64(refs, a, 96);
-                    lds_b32(popped, lds_addr(top), 0);
-                    asm volatile("s_waitcnt lgkmcnt(0)"
-                                 : "+v"(bx0), "+v"(bx1), "+v"(by0), "+v"(by1), "+v"(bz0), "+v"(bz1), "+v"(refs),
-                                   "+v"(popped));
-                    ref0 = refs.x;
-                    ref1 = refs.y;
-                } else {
-                    const char* nb = (const char*)nodes + cur;  // byte-offset ref
-                    bx0 = *(const f2*)(nb + ax); by0 = *(const f2*)(nb + ay); bz0 = *(const f2*)(nb + az);
-                    bx1 = *(const f2*)(nb + 48 + ax); by1 = *(const f2*)(nb + 48 + ay); bz1 = *(const f2*)(nb + 48 + az);
-                    ref0 = *(const int32_t*)(nb + 96);
-                    ref1 = *(const int32_t*)(nb + 100);
-                    popped = *top;
-                }
-                const f2 tx0 = pk_fma_lo(bx0, inv_x, noi_x);
-                const f2 ty0 = pk_fma_lo(by0, inv_y, noi_y);
-                const f2 tz0 = pk_fma_lo(bz0, inv_z, noi_z);
-                const f2 tx1 = pk_fma_lo(bx1, inv_x, noi_x);
-                const f2 ty1 = pk_fma_lo(by1, inv_y, noi_y);
-                const f2 tz1 = pk_fma_lo(bz1, inv_z, noi_z);
-                const float n0 = slab_near(tx0.x, ty0.x, tz0.x, lower), f0 = slab_far(tx0.y, ty0.y, tz0.y, upper);
-                const float n1 = slab_near(tx1.x, ty1.x, tz1.x, lower), f1 = slab_far(tx1.y, ty1.y, tz1.y, upper);
-                // both hit: descend into the nearer child and push the farther one (the store
-                // always happens; it only counts when sp advances); one hit: descend; none: pop.
-                // The three compares are taken as wave masks and combined on the scalar unit, and
-                // the selects are v_cndmask on those masks: 3 compares + 5 selects (the compiler's
-                // form of the same logic re-compared a negated mask on the VALU).
-                const uint64_t m0 = __ballot(n0 <= f0), m1 = __ballot(n1 <= f1), mf = __ballot(n0 <= n1);
-                const uint64_t pick0 = m0 & (~m1 | mf);  // both: nearer; one: that one
-                const uint64_t any = m0 | m1, both = m0 & m1;
-                const int32_t near = sel_mask(ref1, ref0, pick0), far = sel_mask(ref0, ref1, pick0);
-                top[kBlockBvh] = far;
-                cur = sel_mask(popped, near, any);
-                top += sel_mask(sel_mask(-kBlockBvh, 0, any), kBlockBvh, both);
-            }
-            if (cur != kDone) {
+        while (cur != kEnd) {
+            descend(cur, top, ax, ay, az, inv_x, inv_y, inv_z, noi_x, noi_y, noi_z, lower, upper, pr);
+            if (cur != kEnd) {
                 pr.leaf_iter();
                 // leaf: exactly kLeafBvh slots (sentinel-padded); the kLeafBvh discriminant chains
                 // are independent, the candidate updates then run in slot order
@@ -639,17 +929,17 @@ struct BvhWalker {
                 pr.tests(kLeafBvh);
                 upper = (float)closest;
                 upper = upper + __builtin_fabsf(upper) * 0x1p-20f;
-                cur = *top;  // pop (entry 0: kDone)
-                top -= kBlockBvh;
+                cur = *top;  // pop (entry 0: kEnd)
+                top -= kStride;
             }
             if constexpr (kSusp) {
                 // wave-uniform: enough free lanes to make a shading batch worthwhile
-                const uint64_t walking = __ballot(cur != kDone);
+                const uint64_t walking = __ballot(cur != kEnd);
                 if (walking != 0 && 64 - __popcll(walking) >= kRefetchK) break;
             }
         }
         if constexpr (kSusp) {
-            if (cur != kDone) {
+            if (cur != kEnd) {
                 st.cur = cur;
                 st.top = top;
                 st.closest = closest;
@@ -662,6 +952,102 @@ struct BvhWalker {
         return found ? (int)best : -1;
     }
 };
+
+// Fast mode's pieces of the path loop (the parity forms are written inline there).
+template <class W, class = void>
+struct WalkerPrecision {
+    static constexpr bool kF32 = false;
+};
+template <class W>
+struct WalkerPrecision<W, std::void_t<decltype(W::kFast)>> {
+    static constexpr bool kF32 = W::kFast;
+};
+// one trip of the shared rejection loop: randomUnitVec (3 draws) or randomInUnitDisk (2 draws)
+__device__ __forceinline__ void trip_f32(Rng& g, bool wr, float& ux, float& uy, float& uz, float& uls, bool& got,
+                                         bool& dgot) {
+#pragma clang fp contract(fast)
+    fm::uniform2(g, ux, uy);
+    ux = fm::pm1(ux);
+    uy = fm::pm1(uy);
+    const float xy = ux * ux + uy * uy;
+    if (wr) {
+        uz = fm::pm1(fm::uniform(g));
+        uls = xy + uz * uz;
+        got = 1e-30f < uls && uls <= 1.0f;
+    } else {
+        dgot = xy < 1.0f;
+    }
+}
+// the accepted randomUnitVec finishes a Lambertian / Metal scatter (material.zig:27-68)
+__device__ __forceinline__ void scatter_f32(float ux, float uy, float uz, float uls, bool sc_metal, fm::f3 sc_nrm,
+                                            fm::f3 sc_refl, float sc_fuzz, bool& pending, bool& done, fm::Ray& r,
+                                            uint32_t& bounce) {
+#pragma clang fp contract(fast)
+    const fm::f3 ruv = fm::muls(fm::mk(ux, uy, uz), __builtin_amdgcn_rsqf(uls));
+    fm::f3 dir;
+    bool absorbed = false;
+    if (!sc_metal) {
+        dir = fm::add(sc_nrm, ruv);
+        if (fm::near_zero(dir)) dir = sc_nrm;
+    } else {
+        dir = fm::add(sc_refl, fm::muls(ruv, sc_fuzz));
+        absorbed = !(fm::dot(dir, sc_nrm) > 0);
+    }
+    pending = false;
+    if (absorbed) {
+        done = true;
+    } else {
+        r.dir = dir;
+        ++bounce;
+    }
+}
+// rayColor's loop body after the walk (camera.zig:157-177) in f32
+__device__ __forceinline__ void shade_f32(int k, float t, const GeoRec* __restrict__ geo_orig,
+                                          const MatRec* __restrict__ mat_g, Rng& g, fm::Ray& r, fm::f3& att, fm::f3& col,
+                                          bool& done, bool& pending, bool& sc_metal, float& sc_fuzz, fm::f3& sc_nrm,
+                                          fm::f3& sc_refl, uint32_t& bounce) {
+#pragma clang fp contract(fast)
+    MatRec m{};
+    fm::f3 pt = fm::mk(0, 0, 0), nrm = fm::mk(0, 0, 0);
+    bool front = false;
+    fm::f3 x = r.dir;
+    uint32_t kind = 0;
+    if (k >= 0) {
+        const GeoRec sg = geo_orig[k];
+        m = mat_g[k];
+        kind = m.kind;
+        pt = fm::add(r.orig, fm::muls(r.dir, t));
+        const fm::f3 outward = fm::muls(fm::sub(pt, fm::mk((float)sg.cx, (float)sg.cy, (float)sg.cz)), (float)m.inv_r);
+        front = fm::dot(r.dir, outward) < 0;
+        nrm = front ? outward : fm::neg(outward);
+        if (kind == 1) x = fm::reflect(r.dir, nrm);
+    }
+    const fm::f3 u = fm::unit(x);
+    if (k < 0) {
+        const float a = 0.5f * (u.y + 1.0f);
+        col = fm::mul(att, fm::add(fm::muls(fm::mk(1, 1, 1), 1.0f - a), fm::muls(fm::mk(0.5f, 0.7f, 1.0f), a)));
+        done = true;
+    } else if (kind <= 1) {
+        att = fm::mul(att, fm::mk((float)m.albedo[0], (float)m.albedo[1], (float)m.albedo[2]));
+        pending = true;
+        sc_metal = kind == 1;
+        sc_fuzz = (float)m.fuzz;
+        sc_nrm = nrm;
+        sc_refl = u;
+        r.orig = pt;
+    } else {
+        const float ri = front ? (float)m.inv_ior : (float)m.ior;
+        const float cos_t = __builtin_fminf(-fm::dot(u, nrm), 1.0f);
+        const float sin_t = __builtin_sqrtf(__builtin_fmaxf(1.0f - cos_t * cos_t, 0.0f));
+        const bool cannot = ri * sin_t > 1.0f;
+        const float r0 = front ? (float)m.r0_front : (float)m.r0_back;
+        const float x1 = 1.0f - cos_t, x2 = x1 * x1;
+        const float approx = r0 + (1.0f - r0) * (x1 * (x2 * x2));
+        r.dir = (cannot || approx > fm::uniform(g)) ? fm::reflect(u, nrm) : fm::refract(u, nrm, ri);
+        r.orig = pt;
+        ++bounce;
+    }
+}
 
 // ------------------------------------------------------------------------------------------------
 // The path state machine shared by every kernel variant: unit refill (rt_units.h) + one ray segment
@@ -676,19 +1062,25 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
     const uint32_t W = p.width;
     const uint32_t lane = lane_id();
     UnitSched<kDirect> us(ua, blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64);
+    // precision of the walk's instantiation: f64 parity, or fast mode (f32; walkers without the
+    // member are f64)
+    constexpr bool kF32 = WalkerPrecision<Walker>::kF32;
+    using RayT = std::conditional_t<kF32, fm::Ray, Ray>;
+    using Real = std::conditional_t<kF32, float, double>;
+    using V = std::conditional_t<kF32, fm::f3, v3>;
 
     // per-lane path state
     bool active = false;
     uint32_t myslot = 0, mi = 0;  // the unit slot and item of the lane's path (its ring position)
     Rng g;
-    Ray r;
-    v3 att = mk(1, 1, 1);
+    RayT r;
+    V att = V{1, 1, 1};
     uint32_t bounce = 0;
     // pending Lambertian/Metal scatter (waiting for its randomUnitVec), see below
     bool pending = false, sc_metal = false;
     bool dpend = false;  // camera ray waiting for its defocus-disk sample (camera_start)
-    double sc_fuzz = 0;
-    v3 sc_nrm = mk(0, 0, 0), sc_refl = mk(0, 0, 0);
+    Real sc_fuzz = 0;
+    V sc_nrm = V{0, 0, 0}, sc_refl = V{0, 0, 0};
     constexpr bool kSusp = kRefetchK > 0 && Walker::kCanSuspend;
     typename Walker::State ws;  // a suspended walk (dynamic fetch, kSusp only)
     bool susp = false;          // this lane's walk is suspended
@@ -722,7 +1114,7 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
             const uint64_t pixel = (uint64_t)j * W + i;
             g.seed(sample_key(p.seed_mix, pixel, fs));
             dpend = camera_start(i, j, g, r);
-            att = mk(1, 1, 1);
+            att = V{1, 1, 1};
             bounce = 0;
         }
         const bool idle = __ballot(active) == 0;
@@ -750,15 +1142,17 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
         // drawing where it stopped.  Every lane consumes its own stream in the reference's order,
         // so the bits do not change.
         bool done = false;
-        v3 col = mk(0, 0, 0);
-        double ux = 0, uy = 0, uz = 0, uls = 1;
+        V col = V{0, 0, 0};
+        Real ux = 0, uy = 0, uz = 0, uls = 1;
         bool got = false, dgot = false;
 #pragma unroll
         for (int trip = 0; trip < kRuvTrips; ++trip) {
             const bool wr = pending && !got, wd = dpend && !dgot;
             const uint64_t need = __ballot(wr || wd);
             if (need == 0) break;
-            if (wr || wd) {
+            if constexpr (kF32) {
+                if (wr || wd) trip_f32(g, wr, ux, uy, uz, uls, got, dgot);
+            } else if (wr || wd) {
                 ux = g.range_pm1();
                 uy = g.range_pm1();
                 const double xy = ux * ux + uy * uy;
@@ -775,7 +1169,9 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
             camera_finish(ux, uy, r);
             dpend = false;
         }
-        if (got) {  // finish the scatter
+        if constexpr (kF32) {
+            if (got) scatter_f32(ux, uy, uz, uls, sc_metal, sc_nrm, sc_refl, sc_fuzz, pending, done, r, bounce);
+        } else if (got) {  // finish the scatter
             const double l = sqrt_normal(uls);  // |p|^2 in (1e-160, 1] (vec.zig:76)
             const SharedRcp rl(l);
             const v3 ruv = mk(rl.div(ux), rl.div(uy), rl.div(uz));  // p / sqrt(|p|^2), true divisions
@@ -807,7 +1203,7 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
             if (bounce >= p.bounce_max) {
                 done = true;  // too many bounces -> black (camera.zig:181)
             } else {
-                double t;
+                Real t;
                 if (!susp) ++rays;
                 uint64_t v0 = 0, t0 = 0;
                 if constexpr (kProf) { v0 = pr.n_visits; t0 = pr.n_tests; }
@@ -819,17 +1215,20 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
                 __builtin_amdgcn_s_setprio(2);
                 int k;
                 if constexpr (kSusp) {
-                    k = walk.template run<true>(r, p.t_min, p.t_max, &t, pr, ws, susp);
+                    k = walk.template run<true>(r, (Real)p.t_min, (Real)p.t_max, &t, pr, ws, susp);
                     susp = k == kSuspended;
                 } else {
-                    k = walk(r, p.t_min, p.t_max, &t, pr);
+                    k = walk(r, (Real)p.t_min, (Real)p.t_max, &t, pr);
                 }
                 __builtin_amdgcn_s_setprio(1);
                 if constexpr (kProf) {
                     if (bounce == 0) { pr.cam_visits += pr.n_visits - v0; pr.cam_tests += pr.n_tests - t0; }
                 }
                 if constexpr (kProf) t_walk1 = __builtin_amdgcn_s_memtime();
-                if (!susp) {  // a suspended walk resumes next iteration; nothing to shade yet
+                if constexpr (kF32) {
+                    if (!susp) shade_f32(k, t, geo_orig, mat_g, g, r, att, col, done, pending, sc_metal, sc_fuzz, sc_nrm,
+                                         sc_refl, bounce);
+                } else if (!susp) {  // a suspended walk resumes next iteration; nothing to shade yet
                 // Three branches below need a unit vector: the sky (unit(ray.dir).y), the
                 // dielectric (unit(ray.dir)) and the metal (unit(reflect(ray.dir, n))).  Each is a
                 // correctly rounded sqrt and division, and a wave executes every branch some lane
@@ -998,18 +1397,25 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kWaves))
 
 // BVH-walk kernel: nodes + slot geometry + slot ids staged in LDS (kLdsScene) or read from global
 // memory; the per-lane traversal stack always lives in LDS.
-template <bool kLdsScene, bool kProf, bool kDirect>
-__global__ __launch_bounds__(kBlockBvh) void sample_kernel_bvh(KernelParams p, BvhArgs b,
-                                                               const GeoRec* __restrict__ geo_g,
-                                                               const MatRec* __restrict__ mat_g, UnitArgs ua,
-                                                               unsigned long long* __restrict__ stats) {
+#ifdef RTZIG_BVH_WAVES
+#define RTK_BVH_WAVES __attribute__((amdgpu_waves_per_eu(RTZIG_BVH_WAVES)))
+#else
+#define RTK_BVH_WAVES
+#endif
+template <bool kLdsScene, bool kProf, bool kDirect, bool kF32>
+__device__ __forceinline__ void bvh_body(const KernelParams& p, const BvhArgs& b, const GeoRec* __restrict__ geo_g,
+                                         const MatRec* __restrict__ mat_g, const UnitArgs& ua,
+                                         unsigned long long* __restrict__ stats) {
     // LDS: [nodes][leaves] (kLdsScene) at address 0, so a node's byte-offset ref IS its LDS
     // address; then the per-lane stacks [kMaxDepthBvh][kBlockBvh]
     extern __shared__ __align__(16) unsigned char lds_raw[];
     const size_t scene_bytes =
         kLdsScene ? (size_t)bvh_leaves_offset(b.n_nodes) + (size_t)b.n_leaves * sizeof(BvhLeaf) : 0;
-    int32_t* stack = (int32_t*)(lds_raw + scene_bytes);
-    stack[threadIdx.x] = kDone;  // entry 0 of this lane's stack: popping it ends the walk
+    // the int16 stack (RTZIG_STACK16) needs every ref in LDS range: the global-memory tree uses int32
+    using Stack = std::conditional_t<kLdsScene, StackEntry, int32_t>;
+    using Walker = BvhWalker<kLdsScene, kBlockBvh, Stack, kF32>;
+    Stack* stack = (Stack*)(lds_raw + scene_bytes);
+    stack[threadIdx.x] = (Stack)Walker::kEnd;  // entry 0 of this lane's stack: popping it ends the walk
     const BvhNode* nodes = b.nodes;
     const BvhLeaf* leaves = b.leaves;
     if constexpr (kLdsScene) {
@@ -1021,9 +1427,25 @@ __global__ __launch_bounds__(kBlockBvh) void sample_kernel_bvh(KernelParams p, B
         nodes = ln;
         leaves = ll;
     }
-    path_loop<kProf, kDirect>(p, BvhWalker<kLdsScene>{nodes, leaves, b.always_geo, b.always_sid, b.n_always, stack + threadIdx.x,
-                                              b.origin_bound, geo_g, p.n_pad}, geo_g,
-                     mat_g, ua, stats);
+    path_loop<kProf, kDirect>(p, Walker{nodes, leaves, b.always_geo, b.always_sid, b.n_always, stack + threadIdx.x,
+                                         b.origin_bound, geo_g, p.n_pad}, geo_g,
+                              mat_g, ua, stats);
+}
+
+template <bool kLdsScene, bool kProf, bool kDirect>
+__global__ __launch_bounds__(kBlockBvh) RTK_BVH_WAVES void sample_kernel_bvh(KernelParams p, BvhArgs b,
+                                                               const GeoRec* __restrict__ geo_g,
+                                                               const MatRec* __restrict__ mat_g, UnitArgs ua,
+                                                               unsigned long long* __restrict__ stats) {
+    bvh_body<kLdsScene, kProf, kDirect, false>(p, b, geo_g, mat_g, ua, stats);
+}
+// Fast mode (RT_PRECISION_F32): the same body in f32; held to the parity kernel's 4 waves per SIMD
+// (left alone its ring-mode instantiation takes 131 VGPRs, i.e. 3 waves)
+template <bool kLdsScene, bool kProf, bool kDirect>
+__global__ __launch_bounds__(kBlockBvh) __attribute__((amdgpu_waves_per_eu(4))) void sample_kernel_fast(
+    KernelParams p, BvhArgs b, const GeoRec* __restrict__ geo_g, const MatRec* __restrict__ mat_g, UnitArgs ua,
+    unsigned long long* __restrict__ stats) {
+    bvh_body<kLdsScene, kProf, kDirect, true>(p, b, geo_g, mat_g, ua, stats);
 }
 
 // Direct mode's second pass (rt_kernel.h "Work units"): thread q adds pixel q's stored colors in
@@ -1172,17 +1594,22 @@ extern "C" hipError_t rtk_launch_samples(const rtk::KernelParams* p, const rtk::
     return hipErrorInvalidValue;
 }
 
-extern "C" hipError_t rtk_launch_samples_bvh(const rtk::KernelParams* p, const rtk::BvhArgs* b,
-                                             const rtk::GeoRec* geo, const rtk::MatRec* mat, const rtk::UnitArgs* ua,
-                                             void* stats, hipStream_t stream, const char** name) {
+namespace {
+template <bool kF32>
+hipError_t launch_bvh(const rtk::KernelParams* p, const rtk::BvhArgs* b, const rtk::GeoRec* geo, const rtk::MatRec* mat,
+                      const rtk::UnitArgs* ua, void* stats, hipStream_t stream, const char** name) {
     using namespace rtk;
     const uint64_t total = (uint64_t)p->n_rows * p->width * p->s_count;
     if (total == 0) return hipSuccess;
     if (b->stack_depth < 2 || b->stack_depth > (uint32_t)kMaxDepthBvh) return hipErrorInvalidValue;
-    const size_t stack_bytes = (size_t)b->stack_depth * kBlockBvh * sizeof(int32_t);
     const size_t scene_bytes = (size_t)bvh_leaves_offset(b->n_nodes) + (size_t)b->n_leaves * sizeof(BvhLeaf);
-    // scene in LDS when two blocks (16 waves) still fit a CU's 160 KiB
-    const bool lds_scene = stack_bytes + scene_bytes <= kLdsSceneBudget;
+    // int16 stack entries (RTZIG_STACK16) hold node and leaf byte offsets below 2^15
+    const bool refs16 = bvh_leaves_offset(b->n_nodes) < 32768u && (size_t)b->n_leaves * sizeof(BvhLeaf) < 32768u;
+    const size_t lds_entry = refs16 ? sizeof(StackEntry) : sizeof(int32_t);
+    // scene in LDS when two blocks still fit a CU's 160 KiB
+    const bool lds_scene = (size_t)b->stack_depth * kBlockBvh * lds_entry + scene_bytes <= kLdsSceneBudget &&
+                           (sizeof(StackEntry) == sizeof(int32_t) || refs16);
+    const size_t stack_bytes = (size_t)b->stack_depth * kBlockBvh * (lds_scene ? sizeof(StackEntry) : sizeof(int32_t));
     const size_t shmem = stack_bytes + (lds_scene ? scene_bytes : 0);
     const uint64_t need = (total + kBlockBvh - 1) / kBlockBvh;
     auto* st = (unsigned long long*)stats;
@@ -1195,18 +1622,40 @@ extern "C" hipError_t rtk_launch_samples_bvh(const rtk::KernelParams* p, const r
         hipLaunchKernelGGL(kernel, dim3(blocks), dim3(kBlockBvh), shmem, stream, *p, *b, geo, mat, *ua, st);
         return hipGetLastError();
     };
-    if (ua->samples != nullptr) {  // direct mode
-        if (p->prof)
-            return lds_scene ? launch(sample_kernel_bvh<true, true, true>, "bvh_lds(prof,direct)")
-                             : launch(sample_kernel_bvh<false, true, true>, "bvh_global(prof,direct)");
-        return lds_scene ? launch(sample_kernel_bvh<true, false, true>, "bvh_lds(direct)")
-                         : launch(sample_kernel_bvh<false, false, true>, "bvh_global(direct)");
+    const bool direct = ua->samples != nullptr;
+    const bool prof = p->prof != 0;
+#define RTK_BVH(L, PR, D, NM)                                                                          \
+    if (lds_scene == L && prof == PR && direct == D) {                                                 \
+        if constexpr (kF32) return launch(sample_kernel_fast<L, PR, D>, NM);                           \
+        else return launch(sample_kernel_bvh<L, PR, D>, NM);                                           \
     }
-    if (p->prof)
-        return lds_scene ? launch(sample_kernel_bvh<true, true, false>, "bvh_lds(prof)")
-                         : launch(sample_kernel_bvh<false, true, false>, "bvh_global(prof)");
-    return lds_scene ? launch(sample_kernel_bvh<true, false, false>, "bvh_lds")
-                     : launch(sample_kernel_bvh<false, false, false>, "bvh_global");
+    if constexpr (kF32) {
+        RTK_BVH(true, true, true, "fast_f32_lds(prof,direct)") RTK_BVH(false, true, true, "fast_f32_global(prof,direct)")
+        RTK_BVH(true, false, true, "fast_f32_lds(direct)") RTK_BVH(false, false, true, "fast_f32_global(direct)")
+        RTK_BVH(true, true, false, "fast_f32_lds(prof)") RTK_BVH(false, true, false, "fast_f32_global(prof)")
+        RTK_BVH(true, false, false, "fast_f32_lds") RTK_BVH(false, false, false, "fast_f32_global")
+    } else {
+        RTK_BVH(true, true, true, "bvh_lds(prof,direct)") RTK_BVH(false, true, true, "bvh_global(prof,direct)")
+        RTK_BVH(true, false, true, "bvh_lds(direct)") RTK_BVH(false, false, true, "bvh_global(direct)")
+        RTK_BVH(true, true, false, "bvh_lds(prof)") RTK_BVH(false, true, false, "bvh_global(prof)")
+        RTK_BVH(true, false, false, "bvh_lds") RTK_BVH(false, false, false, "bvh_global")
+    }
+#undef RTK_BVH
+    return hipErrorInvalidValue;
+}
+}  // namespace
+
+extern "C" hipError_t rtk_launch_samples_bvh(const rtk::KernelParams* p, const rtk::BvhArgs* b,
+                                             const rtk::GeoRec* geo, const rtk::MatRec* mat, const rtk::UnitArgs* ua,
+                                             void* stats, hipStream_t stream, const char** name) {
+    return launch_bvh<false>(p, b, geo, mat, ua, stats, stream, name);
+}
+
+// Fast mode (RT_PRECISION_F32): the same kernel instantiated with kF32 = true.
+extern "C" hipError_t rtk_launch_samples_fast(const rtk::KernelParams* p, const rtk::BvhArgs* b, const rtk::GeoRec* geo,
+                                              const rtk::MatRec* mat, const rtk::UnitArgs* ua, void* stats,
+                                              hipStream_t stream, const char** name) {
+    return launch_bvh<true>(p, b, geo, mat, ua, stats, stream, name);
 }
 
 extern "C" hipError_t rtk_launch_reduce(const rtk::UnitArgs* ua, hipStream_t stream) {

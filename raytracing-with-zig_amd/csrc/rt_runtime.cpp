@@ -307,7 +307,7 @@ bool try_train(SceneData& sd, const rt_camera& cam) {
     // trained tree that would not fit where the SAH tree does (or does not build) is not used
     auto lds_bytes = [](const SceneData& t) {
         return (size_t)rtk::bvh_leaves_offset(t.n_nodes) + (size_t)t.n_leaves * sizeof(rtk::BvhLeaf) +
-               (size_t)t.depth * rtk::kBlockBvh * sizeof(int32_t);
+               (size_t)t.depth * rtk::kBlockBvh * sizeof(rtk::StackEntry);
     };
     SceneData sah_sd = sd;
     set_tree(sah_sd, sah, bound);

@@ -212,7 +212,8 @@ def test_multi_gpu_call_equals_single(oracle, device_map, monkeypatch):
                        out.ctypes.data_as(C.c_void_p))
     assert rc == 0, lib.rt_last_error()
     assert np.array_equal(out[..., :3], ref) and (out[..., 3] == -7.0).all()
-    assert st[0] == rays and st[1] == cam.width * cam.height * 4
+    one, st1 = gpu_render(cam, cam.scene.world, n_gpus=1)
+    assert (st[0], st[1]) == (rays, cam.width * cam.height * 4), (list(st), rays, st1)
     rgb, _ = gpu_render(cam, cam.scene.world, n_gpus=0, output="rgb8")
     assert np.array_equal(rgb, oracle.to_rgb8(ref))
     if device_map is not None:  # the logical device count is what the map says

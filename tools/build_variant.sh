@@ -12,7 +12,6 @@ if [ "$REV" = "WORKTREE" ]; then
     C="$ROOT/raytracing-with-zig_amd/csrc"
     F="-O3 -std=c++17 -fPIC -ffp-contract=off -Wno-unused-function $EXTRA"
     /opt/rocm/bin/hipcc $F -x hip --offload-arch=gfx950 -fno-gpu-rdc -c "$C/rt_kernel.hip" -o "$B/k.o"
-    /opt/rocm/bin/hipcc $F -x hip --offload-arch=gfx950 -fno-gpu-rdc -c "$C/rt_kernel_fast.hip" -o "$B/kf.o"
     /opt/rocm/bin/hipcc $F -x hip --offload-arch=gfx950 -fno-gpu-rdc -c "$C/rt_runtime.cpp" -o "$B/r.o"
     /opt/rocm/bin/hipcc $F -x c++ -c "$C/rt_host.cpp" -o "$B/h.o"
     /opt/rocm/bin/hipcc $F -x c++ -c "$C/rt_bvh.cpp" -o "$B/b.o"
