@@ -20,6 +20,7 @@
 #include <algorithm>
 #include <exception>
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <limits>
@@ -623,10 +624,14 @@ int rt_context_sync(rt_context* ctx) {
     if (rc || !ctx->d_ctr) return rc;
     // the error word is sticky across launches: it reports a failure of ANY render since the last
     // report, and is cleared once reported
+    // (on the context's stream and waited for: hipMemcpy / hipMemset on the null stream are not
+    // ordered with the context's non-blocking streams)
     unsigned long long err = 0;
-    HIP_CHECK(hipMemcpy(&err, ctx->d_ctr + rtk::kErrWord, sizeof err, hipMemcpyDeviceToHost));
+    HIP_CHECK(hipMemcpyAsync(&err, ctx->d_ctr + rtk::kErrWord, sizeof err, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_CHECK(hipStreamSynchronize(ctx->stream));
     if (err) {
-        HIP_CHECK(hipMemset(ctx->d_ctr + rtk::kErrWord, 0, sizeof err));
+        HIP_CHECK(hipMemsetAsync(ctx->d_ctr + rtk::kErrWord, 0, sizeof err, ctx->stream));
+        HIP_CHECK(hipStreamSynchronize(ctx->stream));
         rt_set_last_error(kStallMsg);
         return RT_ERR_HIP;
     }
@@ -712,8 +717,10 @@ int rt_render_rows_async(rt_context* ctx, const rt_camera* cam, uint32_t output_
     if (!rc && !ctx->d_ctr) {
         size_t cb = 0;
         rc = ensure_buffer(ctx, (void**)&ctx->d_ctr, &cb, rtk::kCtrBytes);
-        // the sticky error word starts clear; launches zero only the counters before it
-        if (!rc) HIP_CHECK(hipMemset(ctx->d_ctr, 0, rtk::kCtrBytes));
+        // the sticky error word starts clear; launches zero only the counters before it.  On the
+        // launch stream: a null-stream hipMemset is asynchronous and NOT ordered with this
+        // non-blocking stream, so it could land mid-kernel and reset the claim counters.
+        if (!rc) HIP_CHECK(hipMemsetAsync(ctx->d_ctr, 0, rtk::kCtrBytes, s));
     }
     if (rc) return rc;
     ua.ring = direct ? nullptr : ctx->d_ring;
@@ -986,7 +993,9 @@ int rt_render(const rt_camera* cam, const rt_sphere* spheres, size_t n, const rt
         HIP_CHECK(hipSetDevice(c->device));
         HIP_CHECK(hipStreamSynchronize(c->stream));
         if (c->h_stats[2]) {
-            HIP_CHECK(hipMemset(c->d_ctr + rtk::kErrWord, 0, sizeof(uint64_t)));  // reported: clear the sticky word
+            // reported: clear the sticky word (on the context's stream, see rt_context_sync)
+            HIP_CHECK(hipMemsetAsync(c->d_ctr + rtk::kErrWord, 0, sizeof(uint64_t), c->stream));
+            HIP_CHECK(hipStreamSynchronize(c->stream));
             rt_set_last_error(kStallMsg);
             return RT_ERR_HIP;
         }

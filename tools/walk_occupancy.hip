@@ -53,7 +53,8 @@ struct Segs {  // SoA of the recorded segments, replayed: segment j of the launc
     uint32_t total;   // segments traced by the launch (n x replays)
 };
 
-// One wave-level claim per refill: the needy lanes take consecutive segments (a global counter).
+// Static assignment: lane g of the grid (G lanes) traces segments g, g + G, g + 2G, ... (a shared
+// claim counter would bound the launch at its ~100 atomics per µs, as round 2 measured).
 // The argument order matters: BvhWalker reads the always-list pointers and count from the kernarg
 // segment at BvhArgs's offset in the product kernels (KernelParams first, 336 B, then BvhArgs), so
 // this kernel takes an (unused) KernelParams first as well.
@@ -73,6 +74,8 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(kWaves, kWave
     __syncthreads();
     const W walk{ln, ll, b.always_geo, b.always_sid, b.n_always, stack + threadIdx.x, b.origin_bound, nullptr, 0};
     const uint32_t lane = lane_id();
+    const uint32_t G = gridDim.x * blockDim.x;
+    uint32_t next = blockIdx.x * blockDim.x + threadIdx.x;  // this lane's next segment
     bool active = false, susp = false;
     uint32_t mine = 0;
     Ray r;
@@ -81,23 +84,19 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(kWaves, kWave
     bool drained = false;
     uint64_t check = 0;  // replays: a sum of the results (keeps their work live), compared across variants
     while (true) {
-        const uint64_t needy = __ballot(!active);
-        if (needy && !drained) {
-            uint32_t base = 0;
-            if (lane == 0) base = (uint32_t)atomicAdd(ctr, (unsigned long long)__popcll(needy));
-            base = __builtin_amdgcn_readfirstlane(base);
-            if (!active) {
-                const uint32_t j = base + rank_in(needy);
-                if (j < sg.total) {
-                    const uint32_t i = j < sg.n ? j : j % sg.n;
-                    mine = j;
-                    r.orig = mk(sg.ox[i], sg.oy[i], sg.oz[i]);
-                    r.dir = mk(sg.dx[i], sg.dy[i], sg.dz[i]);
-                    active = true;
-                    susp = false;
-                }
+        if (!active && !drained) {
+            const uint32_t j = next;
+            if (j < sg.total) {
+                const uint32_t i = j < sg.n ? j : j % sg.n;
+                mine = j;
+                r.orig = mk(sg.ox[i], sg.oy[i], sg.oz[i]);
+                r.dir = mk(sg.dx[i], sg.dy[i], sg.dz[i]);
+                active = true;
+                susp = false;
+                next = j + G < j ? 0xffffffffu : j + G;
+            } else {
+                drained = true;
             }
-            if (base + __popcll(needy) >= sg.total) drained = true;
         }
         if (__ballot(active) == 0) break;
         if (active) {
