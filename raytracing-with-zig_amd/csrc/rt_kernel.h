@@ -51,14 +51,13 @@ constexpr uint32_t kSlotMask = (1u << kSlots) - 1;
 constexpr uint32_t kRingSlotDoubles = kUnitS * 64 * 3;
 constexpr uint32_t kRingWaveDoubles = kSlots * kRingSlotDoubles;  // 144 KiB of f64 per wave
 // counters: ring mode's claim counter ctr[0]; direct mode one per queue segment, each on its own
-// 128-B line, ctr[kCtrStride * seg]; the launch's finalised-unit count ctr[kProgWord] (the global
-// progress the bounded waits watch) — all zeroed per launch (the first kCtrLaunchBytes) — then the
-// STICKY error word ctr[kErrWord]: set by a wave that gave up, cleared only by the host after it
-// has reported it (rt_context_sync / rt_render), so a failure in any frame of a run is seen.
+// 128-B line, ctr[kCtrStride * seg] — zeroed per launch (the first kCtrLaunchBytes) — then the
+// STICKY error word ctr[kErrWord]: set by a wave that gave up waiting (rt_units.h), cleared only by
+// the host after it has reported it (rt_context_sync / rt_render), so a failure in any frame of a
+// run is seen.
 constexpr uint32_t kSegs = 8;
 constexpr uint32_t kCtrStride = 16;
-constexpr uint32_t kProgWord = kSegs * kCtrStride;
-constexpr uint32_t kErrWord = kProgWord + kCtrStride;
+constexpr uint32_t kErrWord = kSegs * kCtrStride;
 constexpr size_t kCtrLaunchBytes = (size_t)kErrWord * sizeof(unsigned long long);
 constexpr size_t kCtrBytes = (kErrWord + kCtrStride) * sizeof(unsigned long long);
 constexpr uint64_t kDirectBytes = 2ull << 30;  // direct mode when P x spp x 24 B fits

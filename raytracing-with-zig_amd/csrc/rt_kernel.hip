@@ -1402,42 +1402,41 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kWaves))
 #else
 #define RTK_BVH_WAVES
 #endif
-template <bool kLdsScene, bool kProf, bool kDirect, bool kF32>
-__device__ __forceinline__ void bvh_body(const KernelParams& p, const BvhArgs& b, const GeoRec* __restrict__ geo_g,
-                                         const MatRec* __restrict__ mat_g, const UnitArgs& ua,
-                                         unsigned long long* __restrict__ stats) {
-    // LDS: [nodes][leaves] (kLdsScene) at address 0, so a node's byte-offset ref IS its LDS
-    // address; then the per-lane stacks [kMaxDepthBvh][kBlockBvh]
-    extern __shared__ __align__(16) unsigned char lds_raw[];
-    const size_t scene_bytes =
-        kLdsScene ? (size_t)bvh_leaves_offset(b.n_nodes) + (size_t)b.n_leaves * sizeof(BvhLeaf) : 0;
-    // the int16 stack (RTZIG_STACK16) needs every ref in LDS range: the global-memory tree uses int32
-    using Stack = std::conditional_t<kLdsScene, StackEntry, int32_t>;
-    using Walker = BvhWalker<kLdsScene, kBlockBvh, Stack, kF32>;
-    Stack* stack = (Stack*)(lds_raw + scene_bytes);
-    stack[threadIdx.x] = (Stack)Walker::kEnd;  // entry 0 of this lane's stack: popping it ends the walk
-    const BvhNode* nodes = b.nodes;
-    const BvhLeaf* leaves = b.leaves;
-    if constexpr (kLdsScene) {
-        BvhNode* ln = (BvhNode*)lds_raw;
-        BvhLeaf* ll = (BvhLeaf*)(lds_raw + bvh_leaves_offset(b.n_nodes));
-        for (uint32_t k = threadIdx.x; k < b.n_nodes; k += blockDim.x) ln[k] = b.nodes[k];
-        for (uint32_t k = threadIdx.x; k < b.n_leaves; k += blockDim.x) ll[k] = b.leaves[k];
-        __syncthreads();
-        nodes = ln;
-        leaves = ll;
-    }
-    path_loop<kProf, kDirect>(p, Walker{nodes, leaves, b.always_geo, b.always_sid, b.n_always, stack + threadIdx.x,
-                                         b.origin_bound, geo_g, p.n_pad}, geo_g,
+// The kernel body, pasted into both entry points below: shared through a __device__ function taking
+// the kernel arguments by reference (or by value) the parity kernel compiled to 51 more instructions
+// (SGPR constants rematerialised in the loop), 0.6% slower.
+#define RTK_BVH_BODY(kF32) \
+    /* LDS: [nodes][leaves] (kLdsScene) at address 0, so a node's byte-offset ref IS its LDS */ \
+    /* address; then the per-lane stacks [kMaxDepthBvh][kBlockBvh] */ \
+    extern __shared__ __align__(16) unsigned char lds_raw[]; \
+    const size_t scene_bytes = \
+        kLdsScene ? (size_t)bvh_leaves_offset(b.n_nodes) + (size_t)b.n_leaves * sizeof(BvhLeaf) : 0; \
+    /* the int16 stack (RTZIG_STACK16) needs every ref in LDS range: the global-memory tree uses int32 */ \
+    using Stack = std::conditional_t<kLdsScene, StackEntry, int32_t>; \
+    using Walker = BvhWalker<kLdsScene, kBlockBvh, Stack, kF32>; \
+    Stack* stack = (Stack*)(lds_raw + scene_bytes); \
+    stack[threadIdx.x] = (Stack)Walker::kEnd;  /* entry 0 of this lane's stack: popping it ends the walk */ \
+    const BvhNode* nodes = b.nodes; \
+    const BvhLeaf* leaves = b.leaves; \
+    if constexpr (kLdsScene) { \
+        BvhNode* ln = (BvhNode*)lds_raw; \
+        BvhLeaf* ll = (BvhLeaf*)(lds_raw + bvh_leaves_offset(b.n_nodes)); \
+        for (uint32_t k = threadIdx.x; k < b.n_nodes; k += blockDim.x) ln[k] = b.nodes[k]; \
+        for (uint32_t k = threadIdx.x; k < b.n_leaves; k += blockDim.x) ll[k] = b.leaves[k]; \
+        __syncthreads(); \
+        nodes = ln; \
+        leaves = ll; \
+    } \
+    path_loop<kProf, kDirect>(p, Walker{nodes, leaves, b.always_geo, b.always_sid, b.n_always, stack + threadIdx.x, \
+                                         b.origin_bound, geo_g, p.n_pad}, geo_g, \
                               mat_g, ua, stats);
-}
 
 template <bool kLdsScene, bool kProf, bool kDirect>
 __global__ __launch_bounds__(kBlockBvh) RTK_BVH_WAVES void sample_kernel_bvh(KernelParams p, BvhArgs b,
                                                                const GeoRec* __restrict__ geo_g,
                                                                const MatRec* __restrict__ mat_g, UnitArgs ua,
                                                                unsigned long long* __restrict__ stats) {
-    bvh_body<kLdsScene, kProf, kDirect, false>(p, b, geo_g, mat_g, ua, stats);
+    RTK_BVH_BODY(false)
 }
 // Fast mode (RT_PRECISION_F32): the same body in f32; held to the parity kernel's 4 waves per SIMD
 // (left alone its ring-mode instantiation takes 131 VGPRs, i.e. 3 waves)
@@ -1445,8 +1444,9 @@ template <bool kLdsScene, bool kProf, bool kDirect>
 __global__ __launch_bounds__(kBlockBvh) __attribute__((amdgpu_waves_per_eu(4))) void sample_kernel_fast(
     KernelParams p, BvhArgs b, const GeoRec* __restrict__ geo_g, const MatRec* __restrict__ mat_g, UnitArgs ua,
     unsigned long long* __restrict__ stats) {
-    bvh_body<kLdsScene, kProf, kDirect, true>(p, b, geo_g, mat_g, ua, stats);
+    RTK_BVH_BODY(true)
 }
+#undef RTK_BVH_BODY
 
 // Direct mode's second pass (rt_kernel.h "Work units"): thread q adds pixel q's stored colors in
 // sample order — pixelColor += rayColor(ray), camera.zig:133-136, from pixelColor = 0 — then

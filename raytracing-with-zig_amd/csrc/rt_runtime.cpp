@@ -72,7 +72,7 @@ constexpr size_t kTrainSamples = RTZIG_TRAIN_SAMPLES;  // build knob
 constexpr uint64_t kTrainSeed = 0x7261792d74726565ull;
 constexpr uint32_t kLinearMaxSpheres = 8;    // scenes this small walk the list (use_bvh)
 constexpr const char* kStallMsg =
-    "render kernel: a wave gave up waiting for a running-sum hand-off (no unit finalised for 40 s)";
+    "render kernel: a wave gave up waiting for a running-sum hand-off (one wait exceeded 40 s)";
 
 }  // namespace
 

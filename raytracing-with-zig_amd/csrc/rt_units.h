@@ -30,16 +30,17 @@ __device__ __forceinline__ void st_wt(double* p, double v) {  // global_store_dw
 }
 
 // A wave that cannot claim and has nothing to trace sleeps between polls.  A bug that broke the
-// dependency chain would otherwise hang the GPU, so a wait is bounded — by GLOBAL progress, not by
-// this wave's own: the launch counts its finalised units in ctr[kProgWord], and a waiting wave
-// gives up only when that count has not moved for kStallTicks of wall clock (s_memrealtime, a
-// constant 100 MHz).  A predecessor unit may legitimately take seconds to trace (a huge scene on
-// the linear walk), but while any wave of the launch finalises anything the wait goes on.  Past
-// the bound the wave reports it in the sticky ctr[kErrWord] and gives up (the host returns
-// RT_ERR_HIP).  The timer restarts whenever this wave claims or finalises a unit.  The clock is kept
-// as its low 32 bits (wrapping differences are exact below 2^32 ticks = 42.9 s); a 64-bit timer
-// cost 12 VGPRs of the path loop through SGPR spills.
-constexpr uint32_t kStallTicks = 40u * 100000000u;  // 40 s without any unit finalised
+// dependency chain would otherwise hang the GPU, so each continuous wait is bounded — by wall clock
+// (s_memrealtime, a constant 100 MHz), not by a count of sleeps: a predecessor unit may legitimately
+// take seconds to trace (a scene too large for the tree, walked linearly: ~100x the final scene's
+// per-ray cost at 70 000 spheres), and a fixed sleep count scaled with nothing.  The clock restarts
+// whenever this wave claims or finalises a unit; past kStallTicks the wave reports it in the
+// sticky ctr[kErrWord] and gives up (the host returns RT_ERR_HIP).  The wait's state is ONE SGPR,
+// as the round-2 sleep counter was: a global-progress bound (every finalisation counted, the count
+// and the clock carried by the waiting wave) cost 1.1-1.7% of the frame through SGPR spills into
+// the walk's VGPRs.  The clock is kept as its low 32 bits (wrapping differences are exact below
+// 2^32 ticks = 42.9 s).
+constexpr uint32_t kStallTicks = 40u * 100000000u;  // 40 s in one wait
 __device__ __forceinline__ uint64_t realtime() { return __builtin_amdgcn_s_memrealtime(); }
 
 
@@ -55,8 +56,7 @@ struct UnitSched {
     uint32_t cur_tile = 0, cur_s0 = 0;
     uint32_t st_u[kSlots];           // unit id held by each slot
     uint32_t spins = 0;              // sleeps in all (diagnostics)
-    uint32_t wait_t0 = 0;            // realtime (low word, | 1) when the current wait last saw global progress (0: not waiting)
-    uint32_t wait_prog = 0;          // ctr[kProgWord] as this wave last read it
+    uint32_t wait_t0 = 0;            // realtime (low word, | 1) when the current wait began (0: not waiting)
     uint32_t seen = 0;               // direct mode: item position after this wave's last claim
     uint32_t waves = 1;              // direct mode: the launch's waves
     uint32_t seg = 0, empty = 0;     // direct mode: segment claimed from; segments found empty
@@ -268,8 +268,6 @@ struct UnitSched {
             if (lane == 0) {
                 if (k + 1 < ua.n_chunks)
                     __hip_atomic_store((gu32*)ua.flags + tile, k + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                // global progress for the bounded waits (no return value: the wave does not wait on it)
-                __hip_atomic_fetch_add((gu64*)ua.ctr + kProgWord, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
             busy &= ~(1u << j);
             wait_t0 = 0;
@@ -281,14 +279,9 @@ struct UnitSched {
     // Nothing to trace in this wave: wait for a dependency (bounded).  False: give up (reported).
     __device__ __forceinline__ bool wait(uint32_t lane) {
         ++spins;
-        uint32_t prog = 0;
-        if (lane == 0)
-            prog = (uint32_t)__hip_atomic_load((gu64*)ua.ctr + kProgWord, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        prog = __builtin_amdgcn_readfirstlane(prog);
         const uint32_t now = (uint32_t)realtime() | 1u;
-        if (wait_t0 == 0 || prog != wait_prog) {
+        if (wait_t0 == 0) {
             wait_t0 = now;
-            wait_prog = prog;
         } else if (now - wait_t0 > kStallTicks) {
             if (lane == 0) atomicOr(ua.ctr + kErrWord, 1ull);
             failed = true;
