@@ -158,7 +158,7 @@ int rt_context_kernel_times(rt_context* ctx, double* sample_ms, double* reduce_m
  * totals restart), so a caller can time many frames without a host sync per frame.
  * *n_launches = the number of sample-kernel launches summed. */
 int rt_context_kernel_times_total(rt_context* ctx, double* sample_ms, double* reduce_ms, uint32_t* n_launches);
-/* Instrumented kernels (diagnostics): when enabled, `d_stats` of rt_render_rows_async must hold 24
+/* Instrumented kernels (diagnostics): when enabled, `d_stats` of rt_render_rows_async must hold 32
  * uint64: {rays, samples, sphere tests executed, BVH node visits, wave-cycles in queue refill,
  * wave-cycles in the closest-hit walk, wave-cycles in shading, wave-iterations of the BVH inner
  * (internal-node) loop, wave-iterations of BVH leaf rounds, wave-level candidate blocks (sqrt +
@@ -166,7 +166,8 @@ int rt_context_kernel_times_total(rt_context* ctx, double* sample_ms, double* re
  * camera rays, [13..15] kernel timeline stamps, [16] wave-cycles in the rejection-trip loop,
  * [17] idle sleeps of waves waiting on a hand-off, [18] deferred unit finalisations (previous chunk
  * of the tile not yet finalised), [19] refills that found no free ring slot, [20] / [21] sum / max over
- * waves of (wave end - the wave's first empty claim), [22] the last wave's first empty claim, 0}.  Counts 0-3 are
+ * waves of (wave end - the wave's first empty claim), [22] the last wave's first empty claim, [23..25]
+ * the parts of [4]: wave-cycles finalising units, handing out items (claims), seeding + getRay; 0...}.  Counts 0-3 are
  * exact and deterministic; the cycles and wave-iteration counts are diagnostics. */
 int rt_context_enable_profile(rt_context* ctx, int enable);
 

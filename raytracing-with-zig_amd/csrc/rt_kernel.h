@@ -60,6 +60,7 @@ constexpr uint32_t kCtrStride = 16;
 constexpr uint32_t kErrWord = kSegs * kCtrStride;
 constexpr size_t kCtrLaunchBytes = (size_t)kErrWord * sizeof(unsigned long long);
 constexpr size_t kCtrBytes = (kErrWord + kCtrStride) * sizeof(unsigned long long);
+constexpr uint32_t kStallTicks = 40u * 100000000u;  // bound on one hand-off wait: 40 s at 100 MHz (rt_units.h)
 constexpr uint64_t kDirectBytes = 2ull << 30;  // direct mode when P x spp x 24 B fits
 
 struct UnitArgs {
@@ -75,7 +76,8 @@ struct UnitArgs {
     uint32_t n_tiles, n_units; // n_units = n_tiles * n_chunks < 2^32 (direct mode: the P * spp items)
     uint32_t n_chunks, spp;
     uint32_t P, out_format;    // pixels of the launch; 0 linear f64, 1 rgb8
-    uint32_t ring_waves, pad;  // ring capacity in waves (the launch never has more)
+    uint32_t ring_waves;       // ring capacity in waves (the launch never has more)
+    uint32_t stall_ticks;      // bound on one continuous hand-off wait, 100 MHz ticks (rt_units.h kStallTicks)
     double scale;              // pixelSamplesScale
 };
 

@@ -1087,6 +1087,7 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
     uint64_t rays = 0, nsamples = 0;
     Prof<kProf> pr;
     uint64_t cyc_refill = 0, cyc_walk = 0, cyc_shade = 0, cyc_trips = 0;  // wave-uniform (kProf only)
+    uint64_t cyc_fin = 0, cyc_hand = 0, cyc_seed = 0;  // parts of cyc_refill: finalise, hand-out, seed + getRay
     uint64_t rt_start = 0, rt_drain = 0;  // s_memrealtime (100 MHz) at start / first empty claim (kProf only)
     if constexpr (kProf) rt_start = __builtin_amdgcn_s_memrealtime();
 
@@ -1097,13 +1098,21 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
         __builtin_amdgcn_s_setprio(2);  // the hand-off's dependent loads (see the walk below)
         const bool progressed = us.finalize_one(us.ready_mask(active, myslot), lane);
         __builtin_amdgcn_s_setprio(0);
+        uint64_t t_fin = 0;
+        if constexpr (kProf) {
+            t_fin = __builtin_amdgcn_s_memtime();
+            cyc_fin += t_fin - t_top;
+        }
         // ---- hand new items to lanes without a path (wave-uniform control flow) ----------------
         bool fresh = false;
         uint32_t fq = 0, fs = 0;  // pixel (launch-local) and sample of a freshly handed item
         const bool was_drained = us.drained;
         us.refill(active, fresh, myslot, mi, fq, fs, lane);
+        uint64_t t_ref = 0;
         if constexpr (kProf) {
             if (us.drained && !was_drained) rt_drain = __builtin_amdgcn_s_memrealtime();
+            t_ref = __builtin_amdgcn_s_memtime();
+            cyc_hand += t_ref - t_fin;
         }
         // the lanes handed an item above start their path: seeding and getRay run once, outside
         // the claim loop, so the generator state and ray are not loop-carried through it
@@ -1117,6 +1126,7 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
             att = V{1, 1, 1};
             bounce = 0;
         }
+        if constexpr (kProf) cyc_seed += __builtin_amdgcn_s_memtime() - t_ref;
         const bool idle = __ballot(active) == 0;
         if (idle) {
             // nothing to trace: finish (no unit left, none held), or claim again next iteration
@@ -1375,6 +1385,9 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
                 atomicAdd(&stats[17], (unsigned long long)us.spins);       // idle-wave sleeps
                 atomicAdd(&stats[18], (unsigned long long)us.n_dep_wait);  // deferred finalisations
                 atomicAdd(&stats[19], (unsigned long long)us.n_no_slot);   // refills without a free slot
+                atomicAdd(&stats[23], (unsigned long long)cyc_fin);        // parts of stats[4]
+                atomicAdd(&stats[24], (unsigned long long)cyc_hand);
+                atomicAdd(&stats[25], (unsigned long long)cyc_seed);
             }
         }
     }

@@ -737,6 +737,13 @@ int rt_render_rows_async(rt_context* ctx, const rt_camera* cam, uint32_t output_
     ua.P = (uint32_t)P;
     ua.out_format = output_format;
     ua.ring_waves = ctx->ring_waves;
+    // test hook RTZIG_STALL_US=<µs>: a shorter bound, so the tests can drive the give-up path (the
+    // sticky error word, RT_ERR_HIP, and the next render succeeding)
+    ua.stall_ticks = rtk::kStallTicks;
+    if (const char* e = std::getenv("RTZIG_STALL_US")) {
+        const double us = std::atof(e);
+        if (us >= 0 && us * 100.0 < (double)rtk::kStallTicks) ua.stall_ticks = (uint32_t)(us * 100.0);
+    }
     ua.scale = cam->pixel_samples_scale;
 
     if (ctx->timing) {

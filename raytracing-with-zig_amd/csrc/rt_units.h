@@ -40,7 +40,6 @@ __device__ __forceinline__ void st_wt(double* p, double v) {  // global_store_dw
 // and the clock carried by the waiting wave) cost 1.1-1.7% of the frame through SGPR spills into
 // the walk's VGPRs.  The clock is kept as its low 32 bits (wrapping differences are exact below
 // 2^32 ticks = 42.9 s).
-constexpr uint32_t kStallTicks = 40u * 100000000u;  // 40 s in one wait
 __device__ __forceinline__ uint64_t realtime() { return __builtin_amdgcn_s_memrealtime(); }
 
 
@@ -282,7 +281,7 @@ struct UnitSched {
         const uint32_t now = (uint32_t)realtime() | 1u;
         if (wait_t0 == 0) {
             wait_t0 = now;
-        } else if (now - wait_t0 > kStallTicks) {
+        } else if (now - wait_t0 > ua.stall_ticks) {
             if (lane == 0) atomicOr(ua.ctr + kErrWord, 1ull);
             failed = true;
             return false;

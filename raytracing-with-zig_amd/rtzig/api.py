@@ -216,7 +216,7 @@ class DeviceRenderer:
         check("rt_context_enable_timing", self.lib.rt_context_enable_timing(self.ctx, int(enable)))
 
     def enable_profile(self, enable=True):
-        """Instrumented kernels: the stats buffer passed to render_rows_async must hold 24 u64."""
+        """Instrumented kernels: the stats buffer passed to render_rows_async must hold 32 u64."""
         check("rt_context_enable_profile", self.lib.rt_context_enable_profile(self.ctx, int(enable)))
 
     def kernel_times(self):

@@ -89,3 +89,40 @@ def test_huge_scene_linear_walk_ring_mode(oracle, monkeypatch):
     ref, rays = oracle.render_b(cam.cam, arr, threads=16)
     assert np.array_equal(out.cpu().numpy(), ref)
     assert int(stats[0]) == rays
+
+
+def test_stalled_handoff_reports_error_and_recovers(oracle, monkeypatch):
+    """The bounded hand-off wait's give-up path (rt_units.h).  With the bound shortened to 0 µs
+    (test hook RTZIG_STALL_US) a wave that has to wait for a predecessor unit gives up on its second
+    poll, sets the sticky error word and leaves; the launch must end (not hang) and report
+    RT_ERR_HIP — through rt_context_sync after it, and through rt_render.  A report clears the word,
+    so the next render with the normal bound succeeds and is bit-exact.  One pixel at 700 spp in
+    ring mode: 700 one-sample units of one tile, finalised strictly in chain order, so many waves
+    wait."""
+    from rtzig.abi import RT_ERR_HIP
+    monkeypatch.setenv("RTZIG_UNIT_MODE", "ring")
+    cam = (rtzig.Camera.builder(1, 1.0).setScene(rtzig.Scene.init(0x5eed).generateWorld())
+           .setDefocusAngle(0.6).setFocusDist(10).setViewport((13, 2, 3), (0, 0, 0), 20)
+           .setSamplesPerPixel(700).build())
+    ref, _ = oracle.render_b(cam.cam, cam.scene.world)
+    r = rtzig.DeviceRenderer(0)
+    r.set_scene(cam.scene.world)
+    out = torch.zeros((1, 1, 3), dtype=torch.float64, device="cuda:0")
+    monkeypatch.setenv("RTZIG_STALL_US", "0")
+    r.render_rows_async(cam.cam, out.data_ptr())
+    r.render_rows_async(cam.cam, out.data_ptr())  # a second failing frame before the report
+    with pytest.raises(RtError) as e:
+        r.sync()
+    assert e.value.code == RT_ERR_HIP
+    r.sync()  # reported once: the sticky word is clear again
+    monkeypatch.delenv("RTZIG_STALL_US")
+    r.render_rows_async(cam.cam, out.data_ptr())
+    r.sync()
+    assert np.array_equal(out.cpu().numpy(), ref)
+    r.close()
+    monkeypatch.setenv("RTZIG_STALL_US", "0")
+    with pytest.raises(RtError) as e:
+        rtzig.render(cam.cam, cam.scene.world, n_gpus=1)
+    assert e.value.code == RT_ERR_HIP
+    monkeypatch.delenv("RTZIG_STALL_US")
+    assert np.array_equal(rtzig.render(cam.cam, cam.scene.world, n_gpus=1), ref)

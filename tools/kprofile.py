@@ -39,7 +39,7 @@ r.enable_timing(True)
 row0, step, n_rows = (0, 1, H) if args.rows is None else tuple(int(x) for x in args.rows.split(":"))
 rows = dict(row0=row0, row_step=step, n_rows=n_rows)
 out = torch.empty((n_rows, W, 3), dtype=torch.float64, device="cuda:0")
-stats = torch.zeros(24, dtype=torch.int64, device="cuda:0")
+stats = torch.zeros(32, dtype=torch.int64, device="cuda:0")
 res = {"config": f"{W}x{H} {args.spp}spp, {len(cam.scene.world)} spheres", "variants": {}}
 for v in args.variants.split():
     os.environ["RTZIG_KERNEL"] = v
@@ -76,7 +76,9 @@ for v in args.variants.split():
                         if s[14] and s[22] else None,
                         "wave_tail_avg (own drain to own end)": round(s[20] / 100 / max(1, res_waves), 1),
                         "wave_tail_max": round(s[21] / 100, 1)},
-        "cycle_split": {"refill": round(s[4] / cyc, 4), "walk": round(s[5] / cyc, 4), "shade": round(s[6] / cyc, 4), "trips": round(s[16] / cyc, 4)},
+        "cycle_split": {"refill": round(s[4] / cyc, 4), "walk": round(s[5] / cyc, 4), "shade": round(s[6] / cyc, 4), "trips": round(s[16] / cyc, 4),
+                        "refill_parts": {"finalise": round(s[23] / cyc, 4), "hand_out": round(s[24] / cyc, 4),
+                                         "seed_and_getRay": round(s[25] / cyc, 4)}},
         "scheduler": {"idle_sleeps": s[17], "deferred_finalisations": s[18], "refills_without_free_slot": s[19]},
         "raw": s,
     }
