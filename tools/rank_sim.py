@@ -13,6 +13,7 @@ Per N:
 Prediction: frame(N) = max_rank kernel + gather; efficiency = frame(1) / (N * frame(N)).
 
     python tools/rank_sim.py --spp 500 --reps 3
+    python tools/rank_sim.py --width 3840 --aspect 1.7777777777777777 --spp 10000 --ns 1 8 --reps 1   # config 5
 """
 import argparse
 import json
@@ -33,9 +34,12 @@ LAUNCH_US = 50.0   # fixed cost of one RCCL gather launch + completion (assumed)
 ap = argparse.ArgumentParser()
 ap.add_argument("--spp", type=int, default=500)
 ap.add_argument("--reps", type=int, default=3)
+ap.add_argument("--width", type=int, default=1200)
+ap.add_argument("--aspect", type=float, default=1.5)
+ap.add_argument("--ns", type=int, nargs="+", default=[1, 2, 4, 8])
 args = ap.parse_args()
 
-cam = rtzig.final_scene_camera(width=1200, aspect_ratio=1.5, spp=args.spp)
+cam = rtzig.final_scene_camera(width=args.width, aspect_ratio=args.aspect, spp=args.spp)
 H, W = cam.height, cam.width
 r = rtzig.DeviceRenderer(0)
 r.set_scene(cam.scene.world)
@@ -54,12 +58,13 @@ def kernel_ms(row0, step, n_rows):
 
 res = {"config": f"{W}x{H} {args.spp}spp", "link_GBps_model": LINK_GBPS, "launch_us_model": LAUNCH_US, "ranks": {}}
 base = None
-for n in (1, 2, 4, 8):
+for n in args.ns:
     R = rdist.rows_per_rank(H, n)
     per_rank = []
     for rank in range(n):
         row0, step, n_rows = rdist.rank_rows(H, rank, n)
         per_rank.append(kernel_ms(row0, step, n_rows))
+        print(f"N={n} rank {rank}: {per_rank[-1]:.3f} ms", file=sys.stderr, flush=True)
     k = max(per_rank)
     gather = 0.0
     if n > 1:
