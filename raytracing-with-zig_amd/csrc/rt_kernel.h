@@ -29,24 +29,15 @@ constexpr uint32_t kMaxLdsSpheres = 2048;  // 64 KiB of LDS geometry; above this
 // writes the framebuffer (scale + optional Color.toRgb).  No per-sample buffer and no reduce pass.
 // Chunks: kUnitS samples each, shrinking towards the end of the launch (rt_schedule.hpp).
 //
-// DIRECT mode, for small launches (Ps x spp x 24 B within kDirectBytes: a rank's rows of a
+// DIRECT mode, for small launches (P x spp x 24 B within kDirectBytes: a rank's rows of a
 // multi-GPU job, the short book scenes): the items are numbered flat and sample-major,
-// t = s * P + q.  The sample layers are split into G FOLD GROUPS (rt_schedule.hpp fold_groups:
-// about spp/8 layers each, the last few shrinking), whose items are claimed one group after the
-// other; each group is split into kSegs contiguous queue segments with a counter each; a wave claims
-// a run from its home segment with one atomic (guided: 1/8 of an even share of what the segment has
-// left, 64 to 2048 items), then from the group's other segments 64 at a time, then moves to the next
-// group.  A lane stores its color write-through at samples[s * Ps + q] (Ps = P rounded up to 16
-// pixels, so no 128-B line holds two layers).  Each wave counts its finished items per group and
-// adds the count to the group's done counter (after draining its stores) once it can hold no more
-// of that group's items.  FOLD unit (g, tile), statically owned by wave (g * n_tiles + tile) mod
-// waves: when group g's counter is full and the tile's flag says groups 0..g-1 are folded, lane l
-// adds the group's stored colors of pixel 64 * tile + l, in sample order, to the pixel's running sum
-// (the ring mode hand-off: sc1 sums, flag) — or, for the last group, writes the framebuffer.  The
-// folds of early groups run while later groups are traced; only the last (small) group's folds
-// remain when tracing ends, so there is no reduce pass.  Small launches have few tiles: ring-mode
-// (tile, chunk) units would either be large (a long drain) or so many that the claim counter's
-// rate (≈88 claims per µs) bounds the launch.
+// t = s * P + q, and split into kSegs contiguous queue segments with a counter each; a wave claims a
+// run from its home segment with one atomic (guided: 1/8 of an even share of what the segment has
+// left, 64 to 2048 items), then from the other segments 64 at a time; a lane stores its color at
+// samples[t], and nothing waits on anything; reduce_kernel then adds every pixel's stored colors
+// in sample order.  Small launches have few
+// tiles: (tile, chunk) units would either be large (a long drain) or so many that the claim
+// counter's rate (≈88 claims per µs) bounds the launch.
 // ------------------------------------------------------------------------------------------------
 #ifndef RTZIG_UNIT_S
 #define RTZIG_UNIT_S 48
@@ -59,33 +50,28 @@ constexpr uint32_t kSlots = RTZIG_SLOTS;   // units a wave holds at once (DESIGN
 constexpr uint32_t kSlotMask = (1u << kSlots) - 1;
 constexpr uint32_t kRingSlotDoubles = kUnitS * 64 * 3;
 constexpr uint32_t kRingWaveDoubles = kSlots * kRingSlotDoubles;  // 144 KiB of f64 per wave
-// counters, each on its own 128-B line: ring mode's claim counter ctr[0]; direct mode one per
-// (fold group, queue segment), ctr[kCtrStride * (g * kSegs + seg)], then the groups' done counters
-// (32-bit, in the low word of ctr[kCtrStride * (kDoneBase + g)]) — zeroed per launch (the first
-// kCtrLaunchBytes) — then the STICKY error word ctr[kErrWord]: set by a wave that gave up waiting
-// (rt_units.h), cleared only by the host after it has reported it (rt_context_sync / rt_render), so
-// a failure in any frame of a run is seen.
+// counters: ring mode's claim counter ctr[0]; direct mode one per queue segment, each on its own
+// 128-B line, ctr[kCtrStride * seg] — zeroed per launch (the first kCtrLaunchBytes) — then the
+// STICKY error word ctr[kErrWord]: set by a wave that gave up waiting (rt_units.h), cleared only by
+// the host after it has reported it (rt_context_sync / rt_render), so a failure in any frame of a
+// run is seen.
 constexpr uint32_t kSegs = 8;
-constexpr uint32_t kMaxGroups = 16;  // fold groups of a direct-mode launch (rt_schedule.hpp fold_groups)
 constexpr uint32_t kCtrStride = 16;
-constexpr uint32_t kDoneBase = kMaxGroups * kSegs;
-constexpr uint32_t kErrWord = (kDoneBase + kMaxGroups) * kCtrStride;
+constexpr uint32_t kErrWord = kSegs * kCtrStride;
 constexpr size_t kCtrLaunchBytes = (size_t)kErrWord * sizeof(unsigned long long);
 constexpr size_t kCtrBytes = (kErrWord + kCtrStride) * sizeof(unsigned long long);
 constexpr uint32_t kStallTicks = 40u * 100000000u;  // bound on one hand-off wait: 40 s at 100 MHz (rt_units.h)
-constexpr uint64_t kDirectBytes = 2ull << 30;  // direct mode when Ps x spp x 24 B fits
-constexpr uint32_t kLayerAlign = 16;           // direct mode: layer stride Ps = P rounded up to this (384 B)
+constexpr uint64_t kDirectBytes = 2ull << 30;  // direct mode when P x spp x 24 B fits
 
 struct UnitArgs {
     double* ring;              // [waves][kSlots][kUnitS * 64][3] wave-private sample colors
     double* sums;              // [P][3] running per-pixel sums (write-through hand-off between waves)
-    uint32_t* flags;           // [n_tiles] chunks (direct mode: fold groups) finalised per tile (zeroed per launch)
+    uint32_t* flags;           // [n_tiles] chunks finalised per tile (zeroed per launch)
     void* out;                 // [P][3] f64 linear or u8 RGB (the last chunk's finalisation)
-    unsigned long long* ctr;   // kCtrBytes: claim counters, group done counters, [kErrWord] error word
-    FastDiv div_tiles;         // u -> (chunk, tile); direct mode: fold unit -> (group, tile)
-    const uint32_t* chunk_s0;  // [n_chunks + 1]: chunk (direct mode: fold group) k covers samples
-                               // [chunk_s0[k], chunk_s0[k + 1])
-    double* samples;           // direct mode: [spp][Ps][3] every sample's color (written through, folded in-kernel)
+    unsigned long long* ctr;   // kCtrBytes: claim counters, [kErrWord] error word
+    FastDiv div_tiles;         // u -> (chunk, tile)
+    const uint32_t* chunk_s0;  // [n_chunks + 1]: chunk k covers samples [chunk_s0[k], chunk_s0[k + 1])
+    double* samples;           // direct mode: [spp][P][3] every sample's color (reduce_kernel sums them)
     FastDiv div_p;             // direct mode: / P, item t -> (sample, pixel)
     uint32_t n_tiles, n_units; // n_units = n_tiles * n_chunks < 2^32 (direct mode: the P * spp items)
     uint32_t n_chunks, spp;
@@ -93,8 +79,6 @@ struct UnitArgs {
     uint32_t ring_waves;       // ring capacity in waves (the launch never has more)
     uint32_t stall_ticks;      // bound on one continuous hand-off wait, 100 MHz ticks (rt_units.h kStallTicks)
     double scale;              // pixelSamplesScale
-    uint32_t Ps;               // direct mode: layer stride of `samples` in pixels (P rounded up to kLayerAlign)
-    uint32_t pad;
 };
 
 // samples [*s0, *s0 + *n) of chunk k (the table is read-only: scalar loads)
@@ -216,8 +200,10 @@ __host__ __device__ inline uint32_t bvh_leaves_offset(uint32_t n_nodes) {
 
 }  // namespace rtk
 
-// Launch wrappers (rt_kernel.hip); asynchronous on `stream`.  The caller zeroes ua->ctr
-// (kCtrLaunchBytes) and ua->flags (n_tiles x 4 B) before every launch.
+// Launch wrappers (rt_kernel.hip, rt_kernel_fast.hip); asynchronous on `stream`.  The caller zeroes
+// ua->ctr (kCtrBytes) and ua->flags (n_tiles x 4 B) before every launch.
+// Direct mode's second pass: per pixel, the stored colors added in sample order, scaled, written.
+extern "C" hipError_t rtk_launch_reduce(const rtk::UnitArgs* ua, hipStream_t stream);
 extern "C" hipError_t rtk_launch_samples(const rtk::KernelParams* p, const rtk::GeoRec* geo,
                                          const rtk::MatRec* mat, const rtk::UnitArgs* ua,
                                          void* stats, hipStream_t stream, const char** name);

@@ -5,16 +5,25 @@
 //     -> HittableList.hit (hittable.zig:64-77) -> Sphere.hit (sphere.zig:26-54)
 //     -> Material.scatter (material.zig:145-151)
 //
-// One persistent kernel per frame: sample_kernel_bvh (BVH walk, the default),
-//   sample_kernel (linear list walk, tiny scenes) or sample_kernel_fast (the BVH kernel in f32).
-//   Waves pull work items (one item = one sample of one pixel) from the unit scheduler
-//   (rt_units.h); a lane whose path ends (miss / absorb / bounceMax) stores the sample's color and
-//   takes the next item in the same iteration, so no lane idles behind a long glass path and no CU
-//   idles behind a slow block.  The per-pixel sums are formed inside the kernel in sample order
-//   (camera.zig:135 `pixelColor += rayColor(ray)`, the same sequence of roundings as the
-//   reference's loop), scaled (camera.zig:137) and written as linear f64 or the fused Color.toRgb
-//   bytes (color.zig:63-80): ring mode by finalising (tile, chunk) units, direct mode by folding
-//   the stored colors group by group while later groups are traced.  There is no second pass.
+// Two kernels (DESIGN.md "Kernels"):
+//
+// sample_kernel — persistent waves pull work items (one item = one sample of one pixel) from a
+//   global queue (8 segments with a counter each, up to 2048 items per wave per atomic).  A lane
+//   whose path ends (miss / absorb / bounceMax) stores the sample's color and immediately takes
+//   the next item, so every lane of
+//   every wave traces one ray segment per loop iteration until the queue drains: no lane idles
+//   behind a long glass path and no CU idles behind a slow block.
+//   Sphere geometry {cx, cy, cz, r^2} is staged once per workgroup into LDS (32 B per sphere);
+//   every lane walks the list in order and all lanes of a wave read the same sphere (LDS
+//   broadcast, conflict-free).  Materials are read from global memory for the hit sphere only.
+//   The closest-hit scan keeps the reference's acceptance rule (strict surrounds on the shrinking
+//   interval) and computes the hit record for the winner only — the same bits as the reference's
+//   per-accepted-sphere record.
+//
+// reduce_kernel — per pixel, adds the stored sample colors in sample order to a running f64 sum
+//   (camera.zig:135 `pixelColor += rayColor(ray)` — the same sequence of roundings as the
+//   reference's loop), then scales by pixelSamplesScale (camera.zig:137) and writes linear f64 or
+//   the fused Color.toRgb bytes (color.zig:63-80).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -1046,13 +1055,13 @@ __device__ __forceinline__ void shade_f32(int k, float t, const GeoRec* __restri
 // samples + the ordered finalisation of finished units.
 // `geo_orig` is the geometry in original list order (hit-record center of the winner).
 // ------------------------------------------------------------------------------------------------
-template <bool kProf, bool kDirect, uint32_t kUaOff, class Walker>
+template <bool kProf, bool kDirect, class Walker>
 __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& walk, const GeoRec* __restrict__ geo_orig,
                                           const MatRec* __restrict__ mat_g, const UnitArgs& ua,
                                           unsigned long long* __restrict__ stats) {
     const uint32_t W = p.width;
     const uint32_t lane = lane_id();
-    UnitSched<kDirect, kUaOff> us(ua, blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64);
+    UnitSched<kDirect> us(ua, blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64);
     // precision of the walk's instantiation: f64 parity, or fast mode (f32; walkers without the
     // member are f64)
     constexpr bool kF32 = WalkerPrecision<Walker>::kF32;
@@ -1062,8 +1071,7 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
 
     // per-lane path state
     bool active = false;
-    uint32_t myslot = 0, mi = 0;  // the unit slot and item of the lane's path (its ring position;
-                                  // direct mode: the item's fold group and store index)
+    uint32_t myslot = 0, mi = 0;  // the unit slot and item of the lane's path (its ring position)
     Rng g;
     RayT r;
     V att = V{1, 1, 1};
@@ -1088,7 +1096,7 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
         if constexpr (kProf) t_top = __builtin_amdgcn_s_memtime();
         // ---- finalise one unit whose samples have all ended (rt_units.h) --------------------------
         __builtin_amdgcn_s_setprio(2);  // the hand-off's dependent loads (see the walk below)
-        const bool progressed = kDirect ? us.fold_step(active, lane) : us.finalize_one(us.ready_mask(active, myslot), lane);
+        const bool progressed = us.finalize_one(us.ready_mask(active, myslot), lane);
         __builtin_amdgcn_s_setprio(0);
         uint64_t t_fin = 0;
         if constexpr (kProf) {
@@ -1121,9 +1129,8 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
         if constexpr (kProf) cyc_seed += __builtin_amdgcn_s_memtime() - t_ref;
         const bool idle = __ballot(active) == 0;
         if (idle) {
-            // nothing to trace: finish (no unit left, none held; direct mode: no fold unit left), or
-            // claim again next iteration
-            if (us.finished()) break;
+            // nothing to trace: finish (no unit left, none held), or claim again next iteration
+            if (us.busy == 0 && us.drained) break;
             // a wave that can neither finalise nor claim waits for the previous chunk of a tile
             // another wave holds
             if (!progressed && !us.can_claim() && !us.wait(lane)) break;
@@ -1303,7 +1310,6 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
             ++nsamples;
             active = false;
         }
-        us.count_done(done, active, myslot, lane);  // direct mode: per-group finished counts
         if constexpr (kProf) {
             // s_memtime is a scalar op: every lane sees the same stamps; lanes that skipped the
             // walk this iteration have t_walk1 == 0 and contribute nothing via the max-reduce below
@@ -1387,27 +1393,6 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
     }
 }
 
-// Kernarg offsets of the UnitArgs argument (rt_units.h karg_at): the kernel arguments are laid out
-// like the members of these structs.
-struct KernArgsLinear {
-    KernelParams p;
-    const GeoRec* geo;
-    const MatRec* mat;
-    UnitArgs ua;
-    unsigned long long* stats;
-};
-struct KernArgsBvh {
-    KernelParams p;
-    BvhArgs b;
-    const GeoRec* geo;
-    const MatRec* mat;
-    UnitArgs ua;
-    unsigned long long* stats;
-};
-constexpr uint32_t kUaOffLinear = offsetof(KernArgsLinear, ua);
-constexpr uint32_t kUaOffBvh = offsetof(KernArgsBvh, ua);
-static_assert(offsetof(KernArgsBvh, b) == 336, "BvhArgs kernarg offset (see BvhWalker's n_always reload)");
-
 // Linear-walk kernel: geometry in LDS (kLds) or read by scalar loads from global memory.
 template <bool kLds, int U, int kWaves, bool kProf, bool kDirect>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kWaves))) void sample_kernel(
@@ -1420,19 +1405,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kWaves))
         __syncthreads();
         geo = lds_geo;
     }
-    path_loop<kProf, kDirect, kUaOffLinear>(p, LinearWalker<U>{geo, p.n_pad, p.n_spheres}, geo, mat_g, ua, stats);
+    path_loop<kProf, kDirect>(p, LinearWalker<U>{geo, p.n_pad, p.n_spheres}, geo, mat_g, ua, stats);
 }
 
 // BVH-walk kernel: nodes + slot geometry + slot ids staged in LDS (kLdsScene) or read from global
 // memory; the per-lane traversal stack always lives in LDS.
-// The uninstrumented kernels are held to 4 waves per SIMD (128 VGPRs): the ring-mode kernel fits
-// by itself (127), the direct-mode one (its folds and counts) needs the bound, which costs it 6
-// VGPR spills, all inside the rare full-range sqrt + reciprocal fallback.  The instrumented ones
-// (kProf, ~165 VGPRs) keep their 3.  Build knob RTZIG_BVH_WAVES overrides the bound.
 #ifdef RTZIG_BVH_WAVES
 #define RTK_BVH_WAVES __attribute__((amdgpu_waves_per_eu(RTZIG_BVH_WAVES)))
 #else
-#define RTK_BVH_WAVES __attribute__((amdgpu_waves_per_eu(kProf ? 3 : 4)))
+#define RTK_BVH_WAVES
 #endif
 // The kernel body, pasted into both entry points below: shared through a __device__ function taking
 // the kernel arguments by reference (or by value) the parity kernel compiled to 51 more instructions
@@ -1459,7 +1440,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kWaves))
         nodes = ln; \
         leaves = ll; \
     } \
-    path_loop<kProf, kDirect, kUaOffBvh>(p, Walker{nodes, leaves, b.always_geo, b.always_sid, b.n_always, stack + threadIdx.x, \
+    path_loop<kProf, kDirect>(p, Walker{nodes, leaves, b.always_geo, b.always_sid, b.n_always, stack + threadIdx.x, \
                                          b.origin_bound, geo_g, p.n_pad}, geo_g, \
                               mat_g, ua, stats);
 
@@ -1479,6 +1460,38 @@ __global__ __launch_bounds__(kBlockBvh) __attribute__((amdgpu_waves_per_eu(4))) 
     RTK_BVH_BODY(true)
 }
 #undef RTK_BVH_BODY
+
+// Direct mode's second pass (rt_kernel.h "Work units"): thread q adds pixel q's stored colors in
+// sample order — pixelColor += rayColor(ray), camera.zig:133-136, from pixelColor = 0 — then
+// scales (:137) and writes linear f64 or the fused Color.toRgb bytes.  A wave's loads of one sample
+// are one contiguous 1536-B run; unrolled 8x to keep loads in flight (the order of the additions
+// is unchanged).
+template <int kOut>
+__global__ __launch_bounds__(256) void reduce_kernel(UnitArgs ua) {
+    const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= ua.P) return;
+    const double* src = ua.samples + 3 * (size_t)q;
+    const size_t stride = 3 * (size_t)ua.P;
+    double x = 0.0, y = 0.0, z = 0.0;
+#pragma unroll 8
+    for (uint32_t s = 0; s < ua.spp; ++s) {
+        x = x + src[0];
+        y = y + src[1];
+        z = z + src[2];
+        src += stride;
+    }
+    if constexpr (kOut == 0) {
+        double* o = (double*)ua.out + 3 * (size_t)q;
+        o[0] = x * ua.scale;
+        o[1] = y * ua.scale;
+        o[2] = z * ua.scale;
+    } else {
+        uint8_t* o = (uint8_t*)ua.out + 3 * (size_t)q;
+        o[0] = to_byte(x * ua.scale);
+        o[1] = to_byte(y * ua.scale);
+        o[2] = to_byte(z * ua.scale);
+    }
+}
 
 }  // namespace rtk
 
@@ -1656,4 +1669,15 @@ extern "C" hipError_t rtk_launch_samples_fast(const rtk::KernelParams* p, const 
                                               const rtk::MatRec* mat, const rtk::UnitArgs* ua, void* stats,
                                               hipStream_t stream, const char** name) {
     return launch_bvh<true>(p, b, geo, mat, ua, stats, stream, name);
+}
+
+extern "C" hipError_t rtk_launch_reduce(const rtk::UnitArgs* ua, hipStream_t stream) {
+    using namespace rtk;
+    if (ua->P == 0 || ua->samples == nullptr) return hipErrorInvalidValue;
+    const uint32_t blocks = (ua->P + 255) / 256;
+    if (ua->out_format == 0)
+        hipLaunchKernelGGL(reduce_kernel<0>, dim3(blocks), dim3(256), 0, stream, *ua);
+    else
+        hipLaunchKernelGGL(reduce_kernel<1>, dim3(blocks), dim3(256), 0, stream, *ua);
+    return hipGetLastError();
 }

@@ -6,8 +6,7 @@
 // a chunk of samples, wave-private rings for the colors of unfinished units, and per-pixel running
 // sums handed from wave to wave behind a per-tile flag.  The workspace is fixed: the rings (144 KiB
 // per wave slot, ≈ 1.2 GB on 256 CUs) plus 24 B of running sum per pixel and 4 B of flag per
-// 64 pixels — independent of spp, and no reduce pass.  Small launches (direct mode) store every
-// sample's color instead and fold them into the running sums group by group inside the same launch.
+// 64 pixels — independent of spp, and no reduce pass.
 //
 // rt_render() keeps one cached context per device for the life of the process (SURVEY §8(b):
 // "an optional rt_context handle caches device init"): the first call creates them on parallel
@@ -92,10 +91,9 @@ struct rt_context {
     size_t sums_bytes = 0;
     uint32_t* d_flags = nullptr;
     size_t flags_bytes = 0;
-    double* d_samples = nullptr;    // direct mode: [spp][Ps][3] (at most rtk::kDirectBytes)
+    double* d_samples = nullptr;    // direct mode: [spp][P][3] (at most rtk::kDirectBytes)
     size_t samples_bytes = 0;
-    std::vector<uint32_t> sched;    // chunk (direct mode: fold group) table of the last launch
-                                    // (rt_schedule.hpp), and its copy
+    std::vector<uint32_t> sched;    // chunk table of the last launch (rt_schedule.hpp), and its copy
     uint32_t* d_sched = nullptr;
     size_t sched_bytes = 0;
     uint64_t sched_lanes = 0;       // resident lanes the schedule is sized for (CUs x 16 waves x 64)
@@ -117,7 +115,7 @@ struct rt_context {
     bool timing = false;
     bool profile = false;  // instrumented kernels: d_stats must hold 24 uint64 (rt.h)
     int precision = RT_PRECISION_F64;
-    std::vector<hipEvent_t> events;  // 3 per timed call: start, sample kernel done, end of the call's work
+    std::vector<hipEvent_t> events;  // 3 per timed call: start, sample kernel done, reduce done
     uint32_t call_first = 0;
     uint32_t timed_calls = 0;
     uint32_t log_used = 0;
@@ -497,12 +495,10 @@ bool use_bvh(const rt_context* ctx) {
     return ctx->scene.bvh_ok;
 }
 
-// Uploads the chunk table of rt_schedule.hpp for `spp` samples over `pixels` — direct mode: the
-// fold groups — (unchanged tables are not re-sent; a changed one waits for the last render, which
-// may still read the old one).
-int upload_schedule(rt_context* ctx, uint32_t spp, uint64_t pixels, bool direct) {
-    std::vector<uint32_t> t =
-        direct ? rtk::fold_groups(spp) : rtk::chunk_schedule(spp, pixels, ctx->sched_lanes, rtk::kUnitS);
+// Uploads the chunk table of rt_schedule.hpp for `spp` samples over `pixels` (unchanged tables are
+// not re-sent; a changed one waits for the last render, which may still read the old one).
+int upload_schedule(rt_context* ctx, uint32_t spp, uint64_t pixels) {
+    std::vector<uint32_t> t = rtk::chunk_schedule(spp, pixels, ctx->sched_lanes, rtk::kUnitS);
     if (ctx->d_sched && t == ctx->sched) return RT_OK;
     int rc = quiesce(ctx);
     if (!rc) rc = ensure_buffer(ctx, (void**)&ctx->d_sched, &ctx->sched_bytes, t.size() * sizeof(uint32_t));
@@ -687,10 +683,17 @@ int rt_render_rows_async(rt_context* ctx, const rt_camera* cam, uint32_t output_
     rtk::UnitArgs ua;
     std::memset(&ua, 0, sizeof ua);
     const uint64_t n_tiles = (P + 63) / 64;
+    rc = upload_schedule(ctx, cam->samples_per_pixel, P);
+    if (rc) return rc;
+    ua.chunk_s0 = ctx->d_sched;
+    ua.n_chunks = (uint32_t)(ctx->sched.size() - 1);
+    if (n_tiles * ua.n_chunks >= (1ull << 32)) {
+        rt_set_last_error("too many work units (rows x samples): render fewer rows per call");
+        return RT_ERR_CAPACITY;
+    }
     // direct mode for small launches (rt_kernel.h "Work units"); RTZIG_UNIT_MODE=ring|direct forces
-    // one (test hook: both paths on the same inputs).  Its layers start on 128-B lines (Ps).
-    const uint64_t Ps = (P + rtk::kLayerAlign - 1) / rtk::kLayerAlign * rtk::kLayerAlign;
-    const uint64_t direct_bytes = Ps * (uint64_t)cam->samples_per_pixel * 3 * sizeof(double);
+    // one (test hook: both paths on the same inputs)
+    const uint64_t direct_bytes = P * (uint64_t)cam->samples_per_pixel * 3 * sizeof(double);
     bool direct = direct_bytes <= rtk::kDirectBytes;
     if (const char* e = std::getenv("RTZIG_UNIT_MODE")) {
         if (std::strcmp(e, "ring") == 0) direct = false;
@@ -702,17 +705,8 @@ int rt_render_rows_async(rt_context* ctx, const rt_camera* cam, uint32_t output_
             direct = true;
         }
     }
-    rc = upload_schedule(ctx, cam->samples_per_pixel, P, direct);
-    if (rc) return rc;
-    ua.chunk_s0 = ctx->d_sched;
-    ua.n_chunks = (uint32_t)(ctx->sched.size() - 1);
-    if (n_tiles * ua.n_chunks >= (1ull << 32)) {
-        rt_set_last_error("too many work units (rows x samples): render fewer rows per call");
-        return RT_ERR_CAPACITY;
-    }
     if (direct) {
         rc = ensure_buffer(ctx, (void**)&ctx->d_samples, &ctx->samples_bytes, direct_bytes);
-        if (!rc && ua.n_chunks > 1) rc = ensure_buffer(ctx, (void**)&ctx->d_sums, &ctx->sums_bytes, P * 3 * sizeof(double));
     } else {
         rc = ensure_buffer(ctx, (void**)&ctx->d_ring, &ctx->ring_bytes,
                            (size_t)ctx->ring_waves * rtk::kRingWaveDoubles * sizeof(double));
@@ -730,7 +724,7 @@ int rt_render_rows_async(rt_context* ctx, const rt_camera* cam, uint32_t output_
     }
     if (rc) return rc;
     ua.ring = direct ? nullptr : ctx->d_ring;
-    ua.sums = ctx->d_sums;
+    ua.sums = direct ? nullptr : ctx->d_sums;
     ua.samples = direct ? ctx->d_samples : nullptr;
     ua.spp = cam->samples_per_pixel;
     ua.flags = ctx->d_flags;
@@ -741,7 +735,6 @@ int rt_render_rows_async(rt_context* ctx, const rt_camera* cam, uint32_t output_
     ua.div_p = rtk::fastdiv_make((uint32_t)P);
     ua.div_tiles = rtk::fastdiv_make((uint32_t)n_tiles);
     ua.P = (uint32_t)P;
-    ua.Ps = (uint32_t)Ps;
     ua.out_format = output_format;
     ua.ring_waves = ctx->ring_waves;
     // test hook RTZIG_STALL_US=<µs>: a shorter bound, so the tests can drive the give-up path (the
@@ -767,7 +760,7 @@ int rt_render_rows_async(rt_context* ctx, const rt_camera* cam, uint32_t output_
     // a previous render of this context on another stream may still use the buffers
     if (ctx->done_valid && ctx->done_stream != s) HIP_CHECK(hipStreamWaitEvent(s, ctx->done, 0));
     HIP_CHECK(hipMemsetAsync(ctx->d_ctr, 0, rtk::kCtrLaunchBytes, s));  // not the sticky error word
-    HIP_CHECK(hipMemsetAsync(ctx->d_flags, 0, flag_bytes, s));
+    if (!direct) HIP_CHECK(hipMemsetAsync(ctx->d_flags, 0, flag_bytes, s));
     const bool bvh = use_bvh(ctx);
     rtk::KernelParams p = make_params(cam, row0, row_step, n_rows, ctx->n_spheres);
     p.prof = ctx->profile && d_stats ? 1u : 0u;
@@ -782,7 +775,8 @@ int rt_render_rows_async(rt_context* ctx, const rt_camera* cam, uint32_t output_
     else
         HIP_CHECK(rtk_launch_samples(&p, ctx->d_geo, ctx->d_mat, &ua, d_stats, s, &ctx->last_kernel));
     if (ev) HIP_CHECK(hipEventRecord(ev[1], s));
-    if (ev) HIP_CHECK(hipEventRecord(ev[2], s));  // (round 2's direct mode ran a reduce pass here)
+    if (direct) HIP_CHECK(rtk_launch_reduce(&ua, s));
+    if (ev) HIP_CHECK(hipEventRecord(ev[2], s));
     HIP_CHECK(hipEventRecord(ctx->done, s));
     ctx->done_valid = true;
     ctx->done_stream = s;
@@ -826,7 +820,7 @@ static int sum_times(rt_context* ctx, uint32_t first, uint32_t count, double* sa
         rm += b;
     }
     if (sample_ms) *sample_ms = sm;
-    if (reduce_ms) *reduce_ms = rm;  // after the sample kernel: empty (round 2: direct mode's reduce pass)
+    if (reduce_ms) *reduce_ms = rm;  // direct mode's reduce pass (ring mode: an empty interval)
     return RT_OK;
 }
 

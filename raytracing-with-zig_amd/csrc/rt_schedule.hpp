@@ -42,31 +42,4 @@ inline std::vector<uint32_t> chunk_schedule(uint32_t spp, uint64_t pixels, uint6
     return s0;
 }
 
-// Direct mode's fold groups (rt_kernel.h "Work units"): s0 of every group plus a final entry ==
-// spp.  A group's folds can only start when its last path has ended, and the launch's last group
-// is folded after tracing has ended, so the groups shrink towards the end: built backwards from
-// max(1, spp / 64) layers, doubling, at most ceil(spp / 8) layers each — at most 12 groups, <=
-// kMaxGroups (config 4 at 500 spp: 17 + 6 x 63 + 56 + 28 + 14 + 7 layers; the last group is folded
-// from 7 x 1.5 KB per wave).
-inline std::vector<uint32_t> fold_groups(uint32_t spp) {
-    const uint32_t cap = std::max<uint32_t>(1, (spp + 7) / 8);
-    uint32_t size = std::max<uint32_t>(1, spp / 64);
-    std::vector<uint32_t> rev;
-    uint32_t after = 0;
-    while (after < spp) {
-        const uint32_t s = std::min(std::min(size, cap), spp - after);
-        rev.push_back(s);
-        after += s;
-        size = size * 2 > cap ? cap : size * 2;
-    }
-    std::vector<uint32_t> s0(rev.size() + 1);
-    uint32_t acc = 0;
-    for (size_t k = 0; k < rev.size(); ++k) {
-        s0[k] = acc;
-        acc += rev[rev.size() - 1 - k];
-    }
-    s0[rev.size()] = acc;
-    return s0;
-}
-
 }  // namespace rtk

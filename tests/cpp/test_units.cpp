@@ -5,7 +5,6 @@
 // obey the drain bound S <= max(1, pixels / (kSchedDiv lanes) * samples_after).  Built with hipcc (host code
 // only; no GPU needed).
 #include <cstdio>
-#include <algorithm>
 #include <cstdlib>
 
 #include "../../raytracing-with-zig_amd/csrc/rt_kernel.h"
@@ -34,35 +33,7 @@ static int check(uint32_t spp, uint64_t pixels, uint64_t lanes) {
     return 0;
 }
 
-// direct mode's fold groups (rt_schedule.hpp fold_groups): tile [0, spp) in order, at most
-// kMaxGroups, no group larger than ceil(spp / 8), sizes non-increasing after the first (the remainder),
-// the last max(1, spp / 64) layers (clamped to what is left)
-static int check_groups(uint32_t spp) {
-    const std::vector<uint32_t> t = rtk::fold_groups(spp);
-    const size_t n = t.size() - 1;
-    if (t.empty() || t[0] != 0 || t[n] != spp || n == 0 || n > rtk::kMaxGroups) {
-        std::printf("fold groups spp %u: bad table (%zu groups)\n", spp, n);
-        return 1;
-    }
-    const uint32_t cap = std::max<uint32_t>(1, (spp + 7) / 8);
-    for (size_t k = 0; k < n; ++k) {
-        const uint32_t sz = t[k + 1] - t[k];
-        if (sz == 0 || sz > cap || (k > 1 && sz > t[k] - t[k - 1])) {
-            std::printf("fold groups spp %u: group %zu has %u layers\n", spp, k, sz);
-            return 1;
-        }
-    }
-    const uint32_t last = t[n] - t[n - 1];
-    if (last != std::min<uint32_t>(std::max<uint32_t>(1, spp / 64), spp)) {
-        std::printf("fold groups spp %u: last group %u layers\n", spp, last);
-        return 1;
-    }
-    return 0;
-}
-
 int main() {
-    for (uint32_t spp = 1; spp <= 20000; ++spp)
-        if (check_groups(spp)) return 1;
     const uint64_t lanes = 256ull * 16 * 64;  // MI355X: 256 CUs x 16 waves
     const uint64_t sizes[] = {1, 37, 1200, 1200 * 100, 1200 * 800, 3840ull * 2160};
     for (uint64_t px : sizes)
