@@ -219,26 +219,46 @@ def run(args):
     renderer = rtzig.DeviceRenderer(local_dev)
     renderer.set_scene(cam.scene.world)
     renderer.enable_timing(True)
-    if args.output == "linear":
-        out = torch.zeros((R, W, 3), dtype=torch.float64, device=dev)
-    else:
-        out = torch.zeros((R, W, 3), dtype=torch.uint8, device=dev)
+    # Two row buffers and a render stream of their own: frame k renders into outs[k % 2] on `stream`
+    # while the collective stream (the current one, which RCCL's gather joins) still gathers frame
+    # k - 1 from the other buffer — the gather overlaps the next frame's render instead of adding to
+    # it.  A buffer is rendered into again only after its previous gather has finished (`freed`).
+    dt = torch.float64 if args.output == "linear" else torch.uint8
+    outs = [torch.zeros((R, W, 3), dtype=dt, device=dev) for _ in range(2)]
+    out = outs[0]
     stats = torch.zeros(2, dtype=torch.int64, device=dev)
-    stream = torch.cuda.current_stream()
+    coll = torch.cuda.current_stream()
+    stream = torch.cuda.Stream(device=dev) if world > 1 else coll
+    rendered = [torch.cuda.Event() for _ in range(2)]
+    freed = [None, None]
+    nframe = [0]
     torch.cuda.synchronize()
     init_ms = (time.perf_counter() - t_init) * 1e3
 
-    def gather():
+    def gather(buf=None):
+        buf = out if buf is None else buf
         if args.dist_backend == "gloo" and world > 1:
-            return rdist.gather_image(out.cpu(), H, rank, world)  # gloo gathers host tensors
-        return rdist.gather_image(out, H, rank, world)
+            return rdist.gather_image(buf.cpu(), H, rank, world)  # gloo gathers host tensors
+        return rdist.gather_image(buf, H, rank, world)
 
     def frame(stats_ptr=None):
+        b = nframe[0] % 2
+        nframe[0] += 1
+        buf = outs[b]
+        if freed[b] is not None:
+            stream.wait_event(freed[b])  # the gather that last read this buffer has finished
         if n_rows:
-            renderer.render_rows_async(cam.cam, out.data_ptr(), row0=row0, row_step=step,
+            renderer.render_rows_async(cam.cam, buf.data_ptr(), row0=row0, row_step=step,
                                        n_rows=n_rows, output=args.output, d_stats_ptr=stats_ptr,
                                        stream_ptr=stream.cuda_stream)
-        return gather()
+        if stream is coll:
+            return gather(buf)
+        rendered[b].record(stream)
+        coll.wait_event(rendered[b])
+        img = gather(buf)
+        freed[b] = torch.cuda.Event()
+        freed[b].record(coll)
+        return img
 
     # the first frame also pays the one-time BVH rebuild from sample rays of this camera (DESIGN.md
     # §5 "Ray-driven tree"): its wall time is reported as a fixed cost
@@ -255,7 +275,7 @@ def run(args):
         renderer.enable_profile(True)
         renderer.render_rows_async(cam.cam, out.data_ptr(), row0=row0, row_step=step, n_rows=n_rows,
                                    output=args.output, d_stats_ptr=pstats.data_ptr(),
-                                   stream_ptr=stream.cuda_stream)
+                                   stream_ptr=coll.cuda_stream)
         torch.cuda.synchronize()
         renderer.enable_profile(False)
     prof = [int(x) for x in pstats.cpu().tolist()]
@@ -379,7 +399,9 @@ def run(args):
                        "spheres": n_spheres, "output": args.output,
                        "parallelism": f"rows interleaved over {world} GPU(s), "
                            + ("RCCL gather to rank 0" if args.dist_backend == "nccl" else
-                              "gloo gather to rank 0 (rehearsal: ranks share devices)")},
+                              "gloo gather to rank 0 (rehearsal: ranks share devices)")
+                           + (", each frame's gather overlapped with the next frame's render (two row buffers)"
+                              if world > 1 else "")},
             "roofline": {
                 "bound": "valu",
                 "kernel": kname,
