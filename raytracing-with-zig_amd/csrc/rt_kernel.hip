@@ -1410,10 +1410,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kWaves))
 
 // BVH-walk kernel: nodes + slot geometry + slot ids staged in LDS (kLdsScene) or read from global
 // memory; the per-lane traversal stack always lives in LDS.
+// The uninstrumented kernels are held to 4 waves per SIMD (128 VGPRs): the LDS-tree kernels fit by
+// themselves (127, 125), the global-tree ring kernel (large scenes) took 133 VGPRs, i.e. 3 waves,
+// and fits 128 with no spill under the bound.  The instrumented ones (kProf, ~160 VGPRs) keep 3.
+// Build knob RTZIG_BVH_WAVES overrides the bound.
 #ifdef RTZIG_BVH_WAVES
 #define RTK_BVH_WAVES __attribute__((amdgpu_waves_per_eu(RTZIG_BVH_WAVES)))
 #else
-#define RTK_BVH_WAVES
+#define RTK_BVH_WAVES __attribute__((amdgpu_waves_per_eu(kProf ? 3 : 4)))
 #endif
 // The kernel body, pasted into both entry points below: shared through a __device__ function taking
 // the kernel arguments by reference (or by value) the parity kernel compiled to 51 more instructions

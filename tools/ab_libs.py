@@ -26,7 +26,9 @@ ap.add_argument("--width", type=int, default=1200)
 ap.add_argument("--aspect", type=float, default=1.5)
 ap.add_argument("--spp", type=int, default=100)
 ap.add_argument("--rounds", type=int, default=5)
-ap.add_argument("--scene", choices=["final", "ch13", "ch9"], default="final")
+ap.add_argument("--scene", choices=["final", "ch13", "ch9", "big"], default="final")
+ap.add_argument("--n-spheres", type=int, default=4000,
+                help="--scene big: random spheres on the final scene's ground (the tree no longer fits LDS)")
 ap.add_argument("--row-step", type=int, default=1,
                 help="render rank 0's interleaved row set of an N-rank job (rows 0, N, 2N, ...)")
 ap.add_argument("--no-check", action="store_true", help="ablation builds: skip the bit-equality check")
@@ -36,8 +38,24 @@ if args.scene == "final":
     cam = rtzig.final_scene_camera(width=args.width, aspect_ratio=args.aspect, spp=args.spp)
 elif args.scene == "ch13":
     cam = rtzig.chapter13_camera(width=args.width, spp=args.spp)
-else:
+elif args.scene == "ch9":
     cam = rtzig.chapter9_camera(width=args.width, spp=args.spp)
+else:  # a scene too large for the LDS tree: the BVH kernel walks its tree in global memory
+    import numpy as np
+    from rtzig.abi import D3, RtSphere
+    rng = np.random.default_rng(4242)
+    n = args.n_spheres
+    arr = (RtSphere * n)()
+    arr[0] = RtSphere(center=D3(0, -1000, 0), radius=1000.0, material=0, albedo=D3(0.5, 0.5, 0.5))
+    c = rng.uniform([-11, 0.05, -11], [11, 0.4, 11], (n, 3))
+    rad = rng.uniform(0.05, 0.2, n)
+    mats = rng.integers(0, 3, n)
+    alb = rng.uniform(0, 1, (n, 3))
+    for k in range(1, n):
+        arr[k] = RtSphere(center=D3(*c[k]), radius=float(rad[k]), material=int(mats[k]), albedo=D3(*alb[k]),
+                          fuzz=0.2, refraction_index=1.5)
+    cam = rtzig.final_scene_camera(width=args.width, aspect_ratio=args.aspect, spp=args.spp)
+    cam.scene.world = arr
 H, W = cam.height, cam.width
 NR = (H + args.row_step - 1) // args.row_step
 out = torch.empty((NR, W, 3), dtype=torch.float64, device="cuda:0")
