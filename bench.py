@@ -138,6 +138,9 @@ def parse_args(argv=None):
     ap.add_argument("--no-dropin", action="store_true", help="skip the rt_render drop-in measurement")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL over xGMI, the product) or gloo (rehearsal: several ranks on one GPU)")
+    ap.add_argument("--check", action="store_true",
+                    help="after the timed region, compare rank 0's last gathered frame bit for bit with "
+                         "a whole-image render on its own device (tests: the pipelined gather path)")
     ap.add_argument("--launch-check", action="store_true",
                     help="start the ranks and join the process group, print one line, render nothing")
     return ap.parse_args(argv)
@@ -304,6 +307,19 @@ def run(args):
     kname = renderer.kernel_name()  # the timed (parity) kernel, before the fast-mode frames
     k_sum, r_sum, n_launch = renderer.kernel_times_total() if n_rows else (0.0, 0.0, 0)
     renderer.sync()  # raises if a wave of any timed frame gave up on a hand-off (sticky error word)
+    check = None
+    if args.check and rank == 0 and n_rows:
+        # the last timed frame as gathered (two row buffers, gather overlapped with the next render)
+        # against one whole-image render on this device: the RNG is keyed by the global pixel, so
+        # they must agree bit for bit
+        whole = torch.empty((H, W, 3), dtype=dt, device=dev)
+        renderer.render_rows_async(cam.cam, whole.data_ptr(), row0=0, row_step=1, n_rows=H, output=args.output,
+                                   stream_ptr=coll.cuda_stream)
+        torch.cuda.synchronize()
+        got = img.cpu() if img is not None else None
+        check = bool(got is not None and torch.equal(got, whole.cpu()))
+        if not check:
+            raise SystemExit("bench.py --check: the gathered frame differs from the whole-image render")
     # N > 1: the gather alone, K times, bracketed like the timed region (the frame's other part)
     coll_dev = dev if args.dist_backend == "nccl" else "cpu"
     gather_ms = 0.0
@@ -449,6 +465,7 @@ def run(args):
                                "first_frame_incl_bvh_training": round(first_ms, 2) if first_ms else None},
             "cpu_baseline": None,
             "fast_f32": fast,
+            **({"check": "gathered frame == whole-image render, bit for bit"} if check else {}),
         }
         if world == 1 and not args.no_dropin and n_rows:
             times = dropin(cam, local_dev)
