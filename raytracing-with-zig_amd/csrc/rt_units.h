@@ -220,8 +220,9 @@ struct UnitSched {
                 continue;
             }
             // Ordering of the hand-off, pinned explicitly rather than by agent-scope acquire/release
-            // (which gfx950 implements as buffer_inv sc1 / buffer_wbl2 sc1: an invalidate or a
-            // write-back of the whole L2 per hand-off).  Hardware: the sums loads below are issued
+            // (gfx950: buffer_inv sc1, an invalidate of this CU's L1 (~1.7 us), and buffer_wbl2 sc1,
+            // a write-back of the XCD L2's dirty lines, per hand-off; MI355X_MICROARCH.md fence
+            // table).  Hardware: the sums loads below are issued
             // only after the flag's value has returned (readfirstlane + the scalar branch above wait
             // for it), and they are sc1 loads; the producer drains its sc1 sum stores
             // (s_waitcnt vmcnt(0)) before its flag store.  Compiler: the fence and the "memory"
