@@ -141,6 +141,10 @@ def parse_args(argv=None):
     ap.add_argument("--check", action="store_true",
                     help="after the timed region, compare rank 0's last gathered frame bit for bit with "
                          "a whole-image render on its own device (tests: the pipelined gather path)")
+    ap.add_argument("--collective", action="store_true",
+                    help="at --gpus 1, still join a (1-rank) process group on --dist-backend and run the "
+                         "N>1 pipeline: two row buffers, the render stream, and each frame's dist.gather on "
+                         "the collective stream (nccl: the RCCL gather on one GPU)")
     ap.add_argument("--launch-check", action="store_true",
                     help="start the ranks and join the process group, print one line, render nothing")
     return ap.parse_args(argv)
@@ -188,7 +192,9 @@ def run(args):
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if args.launch_check:
         # rank plumbing only (CPU tests): join a gloo group, agree on the world size, print it
-        if world > 1:
+        if world > 1 or args.collective:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", str(_free_port()))
             dist.init_process_group("gloo", rank=rank, world_size=world)
             t = torch.tensor([1])
             dist.all_reduce(t)
@@ -207,7 +213,13 @@ def run(args):
     local_dev = local if args.dist_backend == "nccl" else local % max(1, ndev)
     torch.cuda.set_device(local_dev)
     dev = torch.device("cuda", local_dev)
-    if world > 1:
+    # grouped: a process group exists (N > 1, or --collective at N = 1); the pipeline below (render
+    # stream + collective stream, two row buffers, dist.gather per frame) runs whenever it does
+    grouped = world > 1 or args.collective
+    if grouped and world == 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", str(_free_port()))
+    if grouped:
         if args.dist_backend == "nccl":
             dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
         else:
@@ -231,7 +243,7 @@ def run(args):
     out = outs[0]
     stats = torch.zeros(2, dtype=torch.int64, device=dev)
     coll = torch.cuda.current_stream()
-    stream = torch.cuda.Stream(device=dev) if world > 1 else coll
+    stream = torch.cuda.Stream(device=dev) if grouped else coll
     rendered = [torch.cuda.Event() for _ in range(2)]
     freed = [None, None]
     nframe = [0]
@@ -240,9 +252,9 @@ def run(args):
 
     def gather(buf=None):
         buf = out if buf is None else buf
-        if args.dist_backend == "gloo" and world > 1:
-            return rdist.gather_image(buf.cpu(), H, rank, world)  # gloo gathers host tensors
-        return rdist.gather_image(buf, H, rank, world)
+        if args.dist_backend == "gloo" and grouped:
+            return rdist.gather_image(buf.cpu(), H, rank, world, collective=grouped)  # gloo: host tensors
+        return rdist.gather_image(buf, H, rank, world, collective=grouped)
 
     def frame(stats_ptr=None):
         b = nframe[0] % 2
@@ -287,7 +299,7 @@ def run(args):
     # back once after the timed region, so no frame waits on the host
     renderer.enable_timing(True)
 
-    if world > 1:
+    if grouped:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -295,13 +307,13 @@ def run(args):
     for k in range(args.steps):
         img = frame(stats.data_ptr())
     torch.cuda.synchronize()
-    if world > 1:
+    if grouped:
         dist.barrier()
     elapsed = time.perf_counter() - t0
 
     t = torch.tensor([elapsed], dtype=torch.float64,
                      device=dev if args.dist_backend == "nccl" else "cpu")
-    if world > 1:
+    if grouped:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed_max = float(t.item())
     kname = renderer.kernel_name()  # the timed (parity) kernel, before the fast-mode frames
@@ -323,7 +335,7 @@ def run(args):
     # N > 1: the gather alone, K times, bracketed like the timed region (the frame's other part)
     coll_dev = dev if args.dist_backend == "nccl" else "cpu"
     gather_ms = 0.0
-    if world > 1:
+    if grouped:
         dist.barrier()
         torch.cuda.synchronize()
         tg = time.perf_counter()
@@ -334,7 +346,7 @@ def run(args):
         gather_ms = (time.perf_counter() - tg) / args.steps * 1e3
     mine = torch.tensor([float(rank), float(n_rows), k_sum / args.steps, r_sum / args.steps, gather_ms,
                          elapsed / args.steps * 1e3], dtype=torch.float64, device=coll_dev)
-    if world > 1:
+    if grouped:
         every = [torch.zeros_like(mine) for _ in range(world)]
         dist.all_gather(every, mine)
     else:
@@ -401,7 +413,7 @@ def run(args):
             "metric": METRIC,
             "value": round(value, 3),
             "unit": "Msamples/s",
-            "n_gpus": dist.get_world_size() if world > 1 else 1,
+            "n_gpus": dist.get_world_size() if grouped else 1,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(frame_ms, 3),
@@ -413,11 +425,12 @@ def run(args):
                     "seed 0xdeadbeef), main.zig camera preset",
             "config": {"workload": workload, "width": W, "height": H, "spp": spp, "depth": 50,
                        "spheres": n_spheres, "output": args.output,
-                       "parallelism": f"rows interleaved over {world} GPU(s), "
-                           + ("RCCL gather to rank 0" if args.dist_backend == "nccl" else
-                              "gloo gather to rank 0 (rehearsal: ranks share devices)")
-                           + (", each frame's gather overlapped with the next frame's render (two row buffers)"
-                              if world > 1 else "")},
+                       "parallelism": f"rows interleaved over {world} GPU(s)"
+                           + ((", RCCL gather to rank 0" if args.dist_backend == "nccl" else
+                               ", gloo gather to rank 0 (rehearsal: ranks share devices)")
+                              + (" (1-rank group, --collective)" if world == 1 else "")
+                              + ", each frame's gather overlapped with the next frame's render (two row buffers)"
+                              if grouped else "")},
             "roofline": {
                 "bound": "valu",
                 "kernel": kname,
@@ -478,7 +491,7 @@ def run(args):
             res["cpu_baseline"] = cpu_baseline(W, args.aspect, args.cpu_spp)
             res["speedup_vs_cpu_baseline"] = round(value / res["cpu_baseline"]["value"], 1)
         print(json.dumps(res), flush=True)
-    if world > 1:
+    if grouped:
         dist.destroy_process_group()
 
 

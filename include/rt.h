@@ -30,6 +30,8 @@ extern "C" {
 #endif
 
 #define RT_ABI_VERSION 3
+/* uint64 words of the d_stats buffer of an instrumented render (rt_context_enable_profile) */
+#define RT_PROFILE_STATS_WORDS 32
 
 /* ---- status codes ---------------------------------------------------------------------------- */
 typedef enum rt_status {
@@ -110,10 +112,19 @@ typedef struct rt_options {
  * `pixel_stride` doubles (first 3 are r,g,b); RGB8: W*H*3 bytes.  Blocks the calling thread.
  * The library keeps one device context per GPU for the life of the process (created on first use,
  * on parallel host threads): a later call on the same sphere list re-uploads and rebuilds nothing.
- * Its workspace is fixed per device: ≈ 1.2 GB of wave rings plus 24 B per pixel (the kernel
- * accumulates every pixel's samples in order itself); launches whose samples fit 2 GiB instead
- * store them (at most 2 GiB) and sum them in order in a second pass.  Calls are serialised by
- * an internal lock.                                                                               */
+ * Calls are serialised by an internal lock.
+ *
+ * Workspace (per device, held by the cached context; rt_context_workspace_bytes reports it).  A
+ * context holds the buffers of ONE of two modes at a time (switching frees the other's):
+ *   ring mode (launches whose samples need more than 2 GiB, e.g. config 4's full 1200x800x500
+ *   frame on one GPU): one 144-KiB ring per resident wave of the launched kernel (the BVH kernels
+ *   run 16 waves per CU: 576 MiB on a 256-CU MI355X) + 24 B of running sum per pixel + 4 B of flag
+ *   per 64 pixels — config 4: 576 MiB + 22 MiB;
+ *   direct mode (smaller launches: a rank's rows of a multi-GPU job, the 400x225 book scenes): every
+ *   sample's colour, P x spp x 24 B (at most 2 GiB; a rank's 100 rows of config 4 at N = 8:
+ *   1.34 GiB), summed in order by a second pass.
+ * A buffer more than 25% larger than the current launch needs is given back and reallocated.
+ * Plus the framebuffer rows (W x rows x 24 B) and the scene (≈ 100 KB for 485 spheres). */
 int rt_render(const rt_camera* cam, const rt_sphere* spheres, size_t n_spheres,
               const rt_options* opts, void* out);
 /* Frees rt_render's cached device contexts (optional; the next rt_render creates them again). */
@@ -148,6 +159,9 @@ int rt_context_sync(rt_context* ctx);
 int rt_context_set_precision(rt_context* ctx, int precision);
 /* Name of the kernel variant the context launches (for profiling / logs). */
 const char* rt_kernel_name(rt_context* ctx);
+/* Device bytes the context's render workspace holds now (rings, sums, flags, direct-mode samples,
+ * schedule, counters; not the scene or caller buffers): see rt_render "Workspace". */
+int rt_context_workspace_bytes(rt_context* ctx, uint64_t* bytes);
 /* Optional kernel timing with HIP events recorded on the launch stream around the kernels of every
  * render call.  rt_context_kernel_times waits for the last event and returns the durations (ms) of
  * the most recent rt_render_rows_async call: the sample kernel, and the reduce pass of direct mode
@@ -158,8 +172,8 @@ int rt_context_kernel_times(rt_context* ctx, double* sample_ms, double* reduce_m
  * totals restart), so a caller can time many frames without a host sync per frame.
  * *n_launches = the number of sample-kernel launches summed. */
 int rt_context_kernel_times_total(rt_context* ctx, double* sample_ms, double* reduce_ms, uint32_t* n_launches);
-/* Instrumented kernels (diagnostics): when enabled, `d_stats` of rt_render_rows_async must hold 32
- * uint64: {rays, samples, sphere tests executed, BVH node visits, wave-cycles in queue refill,
+/* Instrumented kernels (diagnostics): when enabled, `d_stats` of rt_render_rows_async must hold
+ * RT_PROFILE_STATS_WORDS (32) uint64: {rays, samples, sphere tests executed, BVH node visits, wave-cycles in queue refill,
  * wave-cycles in the closest-hit walk, wave-cycles in shading, wave-iterations of the BVH inner
  * (internal-node) loop, wave-iterations of BVH leaf rounds, wave-level candidate blocks (sqrt +
  * root division), wave-level second-root divisions, node visits of camera rays, sphere tests of

@@ -58,9 +58,15 @@ constexpr uint32_t kRingWaveDoubles = kSlots * kRingSlotDoubles;  // 144 KiB of 
 constexpr uint32_t kSegs = 8;
 constexpr uint32_t kCtrStride = 16;
 constexpr uint32_t kErrWord = kSegs * kCtrStride;
+constexpr unsigned long long kErrStall = 1;   // error-word bits: a hand-off wait gave up (rt_units.h)
+constexpr unsigned long long kErrBounds = 2;  // ... an index out of range (RTZIG_BOUNDS debug builds)
 constexpr size_t kCtrLaunchBytes = (size_t)kErrWord * sizeof(unsigned long long);
 constexpr size_t kCtrBytes = (kErrWord + kCtrStride) * sizeof(unsigned long long);
-constexpr uint32_t kStallTicks = 40u * 100000000u;  // bound on one hand-off wait: 40 s at 100 MHz (rt_units.h)
+// bound on one hand-off wait (rt_units.h wait_clock): units of 256 ticks of the 100 MHz clock
+constexpr double kStallUnitUs = 2.56;
+constexpr uint32_t kStallUnitsPerSec = 390625;  // 1 s / 2.56 µs
+constexpr uint32_t kStallBaseSec = 40;          // default bound; list walks scale it (rt_runtime.cpp)
+constexpr uint32_t kStallMaxSec = 10000;        // < 2^32 units
 constexpr uint64_t kDirectBytes = 2ull << 30;  // direct mode when P x spp x 24 B fits
 
 struct UnitArgs {
@@ -77,7 +83,7 @@ struct UnitArgs {
     uint32_t n_chunks, spp;
     uint32_t P, out_format;    // pixels of the launch; 0 linear f64, 1 rgb8
     uint32_t ring_waves;       // ring capacity in waves (the launch never has more)
-    uint32_t stall_ticks;      // bound on one continuous hand-off wait, 100 MHz ticks (rt_units.h kStallTicks)
+    uint32_t stall_ticks;      // bound on one continuous hand-off wait, wait_clock units (2.56 µs, rt_units.h)
     double scale;              // pixelSamplesScale
 };
 
@@ -129,7 +135,7 @@ struct KernelParams {
     uint32_t row0, row_step, n_rows, n_spheres;
     uint32_t n_pad;  // n_spheres rounded up to kPad (sentinel-padded)
     uint32_t s_begin, s_count;  // unused by the unit scheduler (kept for the kernarg layout)
-    uint32_t prof;   // 1: instrumented build, stats has 8 entries (see rt_context_enable_profile)
+    uint32_t prof;   // 1: instrumented build, stats holds RT_PROFILE_STATS_WORDS entries (rt.h)
     uint32_t pad2[2];
     FastDiv div_layer;  // / (n_rows * width): item -> (sample, pixel) in the refill
     FastDiv div_width;  // / width: pixel -> (row, column)
@@ -200,20 +206,26 @@ __host__ __device__ inline uint32_t bvh_leaves_offset(uint32_t n_nodes) {
 
 }  // namespace rtk
 
-// Launch wrappers (rt_kernel.hip, rt_kernel_fast.hip); asynchronous on `stream`.  The caller zeroes
-// ua->ctr (kCtrBytes) and ua->flags (n_tiles x 4 B) before every launch.
+// Launch wrappers (rt_kernel.hip); asynchronous on `stream`.  The caller zeroes ua->ctr
+// (kCtrLaunchBytes) and ua->flags (n_tiles x 4 B) before every launch.  `direct`: direct mode
+// (ua->samples set).  With plan_waves != nullptr nothing is launched: *plan_waves receives the waves
+// of the persistent grid the launch would run (resident capacity of the chosen kernel, or fewer for a
+// small launch), before the ring's bound — the runtime sizes the ring to it (ua may be null then).
 // Direct mode's second pass: per pixel, the stored colors added in sample order, scaled, written.
 extern "C" hipError_t rtk_launch_reduce(const rtk::UnitArgs* ua, hipStream_t stream);
 extern "C" hipError_t rtk_launch_samples(const rtk::KernelParams* p, const rtk::GeoRec* geo,
                                          const rtk::MatRec* mat, const rtk::UnitArgs* ua,
-                                         void* stats, hipStream_t stream, const char** name);
+                                         void* stats, hipStream_t stream, const char** name, bool direct,
+                                         uint32_t* plan_waves);
 extern "C" hipError_t rtk_launch_samples_bvh(const rtk::KernelParams* p, const rtk::BvhArgs* b,
                                              const rtk::GeoRec* geo, const rtk::MatRec* mat, const rtk::UnitArgs* ua,
-                                             void* stats, hipStream_t stream, const char** name);
-// Fast mode (rt_kernel_fast.hip): the same persistent path loop and BVH in f32 arithmetic, with
+                                             void* stats, hipStream_t stream, const char** name, bool direct,
+                                             uint32_t* plan_waves);
+// Fast mode: the same persistent path loop and BVH walk instantiated in f32 arithmetic, with
 // the always-list (huge / unboundable) spheres tested in f64.  Statistical parity only.
 extern "C" hipError_t rtk_launch_samples_fast(const rtk::KernelParams* p, const rtk::BvhArgs* b, const rtk::GeoRec* geo,
                                               const rtk::MatRec* mat, const rtk::UnitArgs* ua, void* stats,
-                                              hipStream_t stream, const char** name);
+                                              hipStream_t stream, const char** name, bool direct,
+                                              uint32_t* plan_waves);
 // Resident blocks of `kernel` on the current device (CUs x occupancy), cached (rt_kernel.hip).
 extern "C" hipError_t rtk_resident_blocks(const void* kernel, int block, size_t shmem, uint32_t* blocks);

@@ -457,6 +457,25 @@ struct BvhWalker {
     float origin_bound;                  // BvhArgs::origin_bound
     const GeoRec* __restrict__ geo_all;  // the whole list in original order (far-origin lanes)
     uint32_t n_pad;
+#if RTZIG_BOUNDS
+#ifndef RTZIG_BOUNDS_SELFTEST
+#define RTZIG_BOUNDS_SELFTEST 0  // 1: the tree's last node counts as out of range (the check must report it)
+#endif
+    uint32_t node_bytes, leaf_bytes, depth;  // debug builds: the tree's extent, the stack's entries
+    unsigned long long* err;                 // UnitArgs::ctr (the error word, rt_units.h bounds_ok)
+    __device__ __forceinline__ bool node_ok(int32_t& cur, StackT* top) const {
+        // at an internal node the lane's stack holds entries 0..sp and the push writes entry sp + 1,
+        // which must lie below `depth` (the tree's depth bounds the pushes on any root path)
+        const bool ok = (uint32_t)cur < node_bytes - RTZIG_BOUNDS_SELFTEST * (uint32_t)sizeof(BvhNode) &&
+                        top >= stack && top + kStride < stack + depth * kStride;
+        if (!bounds_ok(ok, err)) cur = kEnd;
+        return ok;
+    }
+    __device__ __forceinline__ bool leaf_ok(int32_t cur) const { return bounds_ok((uint32_t)(~cur) < leaf_bytes, err); }
+#else
+    __device__ __forceinline__ bool node_ok(int32_t&, StackT*) const { return true; }
+    __device__ __forceinline__ bool leaf_ok(int32_t) const { return true; }
+#endif
 
     // always-list sphere q: geometry + original index from global memory (uniform address,
     // read-only data: scalar loads; the compiler emits per-lane vector loads, since it cannot prove
@@ -635,6 +654,7 @@ struct BvhWalker {
                                             f2 inv_x, f2 inv_y, f2 inv_z, f2 noi_x, f2 noi_y, f2 noi_z, float lower,
                                             float upper, PR& pr) const {
         while (cur >= 0) {
+            if (!node_ok(cur, top)) break;
             pr.visit();
             pr.inner_iter();
             f2 bx0, by0, bz0, bx1, by1, bz1;
@@ -736,6 +756,7 @@ struct BvhWalker {
         }
         while (cur != kEnd) {
             descend(cur, top, ax, ay, az, inv_x, inv_y, inv_z, noi_x, noi_y, noi_z, lower, upper, pr);
+            if (cur != kEnd && !leaf_ok(cur)) cur = kEnd;
             if (cur != kEnd) {
                 pr.leaf_iter();
                 leaf_f32((const BvhLeaf*)((const char*)leaves + (uint32_t)(~cur)), r, t_min, inv_a, a, closest, best, found);
@@ -859,6 +880,7 @@ struct BvhWalker {
         // f64 leaf work runs with most lanes active instead of whenever any one lane hits a leaf.
         while (cur != kEnd) {
             descend(cur, top, ax, ay, az, inv_x, inv_y, inv_z, noi_x, noi_y, noi_z, lower, upper, pr);
+            if (cur != kEnd && !leaf_ok(cur)) cur = kEnd;
             if (cur != kEnd) {
                 pr.leaf_iter();
                 // leaf: exactly kLeafBvh slots (sentinel-padded); the kLeafBvh discriminant chains
@@ -1236,6 +1258,7 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
                 }
                 if constexpr (kProf) t_walk1 = __builtin_amdgcn_s_memtime();
                 if constexpr (kF32) {
+                    if (k >= 0 && !bounds_ok((uint32_t)k < p.n_spheres, ua.ctr)) k = -1;
                     if (!susp) shade_f32(k, t, geo_orig, mat_g, g, r, att, col, done, pending, sc_metal, sc_fuzz, sc_nrm,
                                          sc_refl, bounce);
                 } else if (!susp) {  // a suspended walk resumes next iteration; nothing to shade yet
@@ -1256,6 +1279,7 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
                        r0 = __builtin_nondeterministic_value(0.0);
                 uint32_t kind = __builtin_nondeterministic_value(0u);
                 v3 x = r.dir;
+                if (k >= 0 && !bounds_ok((uint32_t)k < p.n_spheres, ua.ctr)) k = -1;
                 if (k >= 0) {
                     const GeoRec sg = geo_orig[k];
                     const MatRec m = mat_g[k];
@@ -1422,6 +1446,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kWaves))
 // The kernel body, pasted into both entry points below: shared through a __device__ function taking
 // the kernel arguments by reference (or by value) the parity kernel compiled to 51 more instructions
 // (SGPR constants rematerialised in the loop), 0.6% slower.
+#if RTZIG_BOUNDS
+#define RTK_BOUNDS_ARGS \
+    , b.n_nodes * (uint32_t)sizeof(BvhNode), (uint32_t)(b.n_leaves * sizeof(BvhLeaf)), b.stack_depth, ua.ctr
+#else
+#define RTK_BOUNDS_ARGS
+#endif
 #define RTK_BVH_BODY(kF32) \
     /* LDS: [nodes][leaves] (kLdsScene) at address 0, so a node's byte-offset ref IS its LDS */ \
     /* address; then the per-lane stacks [kMaxDepthBvh][kBlockBvh] */ \
@@ -1445,7 +1475,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kWaves))
         leaves = ll; \
     } \
     path_loop<kProf, kDirect>(p, Walker{nodes, leaves, b.always_geo, b.always_sid, b.n_always, stack + threadIdx.x, \
-                                         b.origin_bound, geo_g, p.n_pad}, geo_g, \
+                                         b.origin_bound, geo_g, p.n_pad RTK_BOUNDS_ARGS}, geo_g, \
                               mat_g, ua, stats);
 
 template <bool kLdsScene, bool kProf, bool kDirect>
@@ -1548,19 +1578,29 @@ uint32_t persistent_blocks(K kernel, size_t shmem) {
     return b;
 }
 
-// blocks of a persistent launch: resident capacity, the work, and the ring's wave capacity
+// blocks of a persistent launch: resident capacity, the work, and (ring mode) the ring's wave capacity
 uint32_t grid_blocks(uint64_t need, uint64_t cap, const rtk::UnitArgs* ua, uint32_t block) {
-    const uint64_t ring_blocks = ua->ring_waves / (block / 64);
+    const uint64_t ring_blocks = ua->ring ? ua->ring_waves / (block / 64) : UINT64_MAX;
     uint64_t b = need < cap ? need : cap;
     return (uint32_t)(b < ring_blocks ? b : ring_blocks);
 }
 
+// waves of the persistent grid a launch of `need` blocks would have before the ring's bound: the
+// runtime sizes the ring to it (rtk_launch_* with plan_waves != nullptr)
+uint32_t plan_of(uint64_t need, uint64_t cap, uint32_t block) {
+    return (uint32_t)((need < cap ? need : cap) * (block / 64));
+}
+
 template <bool kLds, int U, int kWaves>
 void launch_samples(const rtk::KernelParams* p, const rtk::GeoRec* geo, const rtk::MatRec* mat,
-                    const rtk::UnitArgs* ua, unsigned long long* st, hipStream_t stream, size_t shmem, uint64_t need) {
-    const bool direct = ua->samples != nullptr;
+                    const rtk::UnitArgs* ua, unsigned long long* st, hipStream_t stream, size_t shmem, uint64_t need,
+                    bool direct, uint32_t* plan_waves) {
     auto kernel = p->prof ? (direct ? rtk::sample_kernel<kLds, U, kWaves, true, true> : rtk::sample_kernel<kLds, U, kWaves, true, false>)
                           : (direct ? rtk::sample_kernel<kLds, U, kWaves, false, true> : rtk::sample_kernel<kLds, U, kWaves, false, false>);
+    if (plan_waves) {
+        *plan_waves = plan_of(need, persistent_blocks(kernel, shmem), rtk::kBlock);
+        return;
+    }
     const uint32_t blocks = grid_blocks(need, persistent_blocks(kernel, shmem), ua, rtk::kBlock);
     hipLaunchKernelGGL(kernel, dim3(blocks), dim3(rtk::kBlock), shmem, stream, *p, geo, mat, *ua, st);
 }
@@ -1592,7 +1632,8 @@ const Variant& variant_choice(bool fits_lds, uint32_t n_pad) {
 
 extern "C" hipError_t rtk_launch_samples(const rtk::KernelParams* p, const rtk::GeoRec* geo,
                                          const rtk::MatRec* mat, const rtk::UnitArgs* ua,
-                                         void* stats, hipStream_t stream, const char** name) {
+                                         void* stats, hipStream_t stream, const char** name, bool direct,
+                                         uint32_t* plan_waves) {
     using namespace rtk;
     const uint64_t total = (uint64_t)p->n_rows * p->width * p->s_count;
     if (total == 0) return hipSuccess;
@@ -1603,7 +1644,7 @@ extern "C" hipError_t rtk_launch_samples(const rtk::KernelParams* p, const rtk::
     if (name) *name = v.name;
 #define RTK_CASE(L, U, W)                                                                 \
     if (v.lds == L && v.unroll == U && v.waves == W) {                                   \
-        launch_samples<L, U, W>(p, geo, mat, ua, st, stream, shmem, need);               \
+        launch_samples<L, U, W>(p, geo, mat, ua, st, stream, shmem, need, direct, plan_waves); \
         return hipGetLastError();                                                        \
     }
     RTK_CASE(true, 4, 1) RTK_CASE(false, 4, 1)
@@ -1614,7 +1655,8 @@ extern "C" hipError_t rtk_launch_samples(const rtk::KernelParams* p, const rtk::
 namespace {
 template <bool kF32>
 hipError_t launch_bvh(const rtk::KernelParams* p, const rtk::BvhArgs* b, const rtk::GeoRec* geo, const rtk::MatRec* mat,
-                      const rtk::UnitArgs* ua, void* stats, hipStream_t stream, const char** name) {
+                      const rtk::UnitArgs* ua, void* stats, hipStream_t stream, const char** name, bool direct,
+                      uint32_t* plan_waves) {
     using namespace rtk;
     const uint64_t total = (uint64_t)p->n_rows * p->width * p->s_count;
     if (total == 0) return hipSuccess;
@@ -1634,12 +1676,15 @@ hipError_t launch_bvh(const rtk::KernelParams* p, const rtk::BvhArgs* b, const r
         uint32_t cap32 = 0;
         const hipError_t ea = rtk_resident_blocks((const void*)kernel, kBlockBvh, shmem, &cap32);
         if (ea != hipSuccess) return ea;
+        if (plan_waves) {
+            *plan_waves = plan_of(need, cap32, kBlockBvh);
+            return hipSuccess;
+        }
         const uint32_t blocks = grid_blocks(need, cap32, ua, kBlockBvh);
         if (name) *name = nm;
         hipLaunchKernelGGL(kernel, dim3(blocks), dim3(kBlockBvh), shmem, stream, *p, *b, geo, mat, *ua, st);
         return hipGetLastError();
     };
-    const bool direct = ua->samples != nullptr;
     const bool prof = p->prof != 0;
 #define RTK_BVH(L, PR, D, NM)                                                                          \
     if (lds_scene == L && prof == PR && direct == D) {                                                 \
@@ -1664,15 +1709,17 @@ hipError_t launch_bvh(const rtk::KernelParams* p, const rtk::BvhArgs* b, const r
 
 extern "C" hipError_t rtk_launch_samples_bvh(const rtk::KernelParams* p, const rtk::BvhArgs* b,
                                              const rtk::GeoRec* geo, const rtk::MatRec* mat, const rtk::UnitArgs* ua,
-                                             void* stats, hipStream_t stream, const char** name) {
-    return launch_bvh<false>(p, b, geo, mat, ua, stats, stream, name);
+                                             void* stats, hipStream_t stream, const char** name, bool direct,
+                                             uint32_t* plan_waves) {
+    return launch_bvh<false>(p, b, geo, mat, ua, stats, stream, name, direct, plan_waves);
 }
 
 // Fast mode (RT_PRECISION_F32): the same kernel instantiated with kF32 = true.
 extern "C" hipError_t rtk_launch_samples_fast(const rtk::KernelParams* p, const rtk::BvhArgs* b, const rtk::GeoRec* geo,
                                               const rtk::MatRec* mat, const rtk::UnitArgs* ua, void* stats,
-                                              hipStream_t stream, const char** name) {
-    return launch_bvh<true>(p, b, geo, mat, ua, stats, stream, name);
+                                              hipStream_t stream, const char** name, bool direct,
+                                              uint32_t* plan_waves) {
+    return launch_bvh<true>(p, b, geo, mat, ua, stats, stream, name, direct, plan_waves);
 }
 
 extern "C" hipError_t rtk_launch_reduce(const rtk::UnitArgs* ua, hipStream_t stream) {

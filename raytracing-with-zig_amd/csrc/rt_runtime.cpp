@@ -4,9 +4,11 @@
 // One render of rows = ONE persistent launch of the sample kernel.  It accumulates every pixel's
 // samples in sample order itself (rt_kernel.h "Work units", rt_units.h): work units of 64 pixels x
 // a chunk of samples, wave-private rings for the colors of unfinished units, and per-pixel running
-// sums handed from wave to wave behind a per-tile flag.  The workspace is fixed: the rings (144 KiB
-// per wave slot, ≈ 1.2 GB on 256 CUs) plus 24 B of running sum per pixel and 4 B of flag per
-// 64 pixels — independent of spp, and no reduce pass.
+// sums handed from wave to wave behind a per-tile flag.  The workspace is independent of spp: one
+// 144-KiB ring per resident wave of the kernel actually launched (the BVH kernels: 16 waves per CU,
+// 576 MiB on 256 CUs) plus 24 B of running sum per pixel and 4 B of flag per 64 pixels.  Small
+// launches (direct mode) instead store every sample (at most 2 GiB) for a reduce pass; a context
+// holds the buffers of one mode at a time (rt.h "Workspace").
 //
 // rt_render() keeps one cached context per device for the life of the process (SURVEY §8(b):
 // "an optional rt_context handle caches device init"): the first call creates them on parallel
@@ -40,7 +42,6 @@ void rt_set_last_error(const std::string& msg);
 namespace {
 
 constexpr uint32_t kMaxTimed = 1024;  // event-pool bound of rt_context_kernel_times_total
-constexpr uint32_t kMaxWavesPerCU = 32;  // gfx950: 4 SIMDs x 8 wave slots (the ring's capacity)
 
 // Host-side scene: device records of the Hittable list plus its BVH, built once per sphere list and
 // uploaded to every device that renders it.
@@ -72,7 +73,8 @@ constexpr size_t kTrainSamples = RTZIG_TRAIN_SAMPLES;  // build knob
 constexpr uint64_t kTrainSeed = 0x7261792d74726565ull;
 constexpr uint32_t kLinearMaxSpheres = 8;    // scenes this small walk the list (use_bvh)
 constexpr const char* kStallMsg =
-    "render kernel: a wave gave up waiting for a running-sum hand-off (one wait exceeded 40 s)";
+    "render kernel: a wave gave up waiting for a running-sum hand-off (one wait exceeded its bound: 40 s, "
+    "scaled with the sphere count for list walks)";
 
 }  // namespace
 
@@ -86,7 +88,7 @@ struct rt_context {
     // workspace (rt_kernel.h "Work units"): wave rings, running sums, per-tile flags, counters
     double* d_ring = nullptr;
     size_t ring_bytes = 0;
-    uint32_t ring_waves = 0;
+    uint32_t ring_waves = 0;        // waves the ring holds (sized to the launched kernel's grid)
     double* d_sums = nullptr;
     size_t sums_bytes = 0;
     uint32_t* d_flags = nullptr;
@@ -113,7 +115,7 @@ struct rt_context {
     hipStream_t done_stream = nullptr;
     // optional kernel timing: an event pair around every launch
     bool timing = false;
-    bool profile = false;  // instrumented kernels: d_stats must hold 24 uint64 (rt.h)
+    bool profile = false;  // instrumented kernels: d_stats must hold RT_PROFILE_STATS_WORDS uint64 (rt.h)
     int precision = RT_PRECISION_F64;
     std::vector<hipEvent_t> events;  // 3 per timed call: start, sample kernel done, reduce done
     uint32_t call_first = 0;
@@ -394,6 +396,30 @@ int ensure_buffer(rt_context* ctx, void** ptr, size_t* bytes, size_t need) {
     return RT_OK;
 }
 
+// ensure_buffer that also gives memory back: a buffer more than 25% larger than `need` (held for
+// an earlier, larger launch or a kernel with more resident waves) is reallocated at `need`
+int fit_buffer(rt_context* ctx, void** ptr, size_t* bytes, size_t need) {
+    if (*ptr && *bytes > need + need / 4) {
+        int rc = quiesce(ctx);
+        if (rc) return rc;
+        (void)hipFree(*ptr);
+        *ptr = nullptr;
+        *bytes = 0;
+    }
+    return ensure_buffer(ctx, ptr, bytes, need);
+}
+
+// Frees a workspace buffer the current launch's mode does not use (after the last render).
+int release_buffer(rt_context* ctx, void** ptr, size_t* bytes) {
+    if (!*ptr) return RT_OK;
+    int rc = quiesce(ctx);
+    if (rc) return rc;
+    (void)hipFree(*ptr);
+    *ptr = nullptr;
+    *bytes = 0;
+    return RT_OK;
+}
+
 template <class T>
 int upload(rt_context* ctx, T** dptr, size_t* bytes, const std::vector<T>& v) {
     int rc = ensure_buffer(ctx, (void**)dptr, bytes, v.size() * sizeof(T));
@@ -549,6 +575,29 @@ rtk::KernelParams make_params(const rt_camera* c, uint32_t row0, uint32_t row_st
     return p;
 }
 
+// The sticky error word's message (rt_units.h: bit 0 a hand-off wait gave up; bit 1, debug builds
+// only, an index out of range)
+std::string err_message(unsigned long long err) {
+    std::string m;
+    if (err & rtk::kErrBounds) m = "render kernel: an index out of range (RTZIG_BOUNDS debug build)";
+    if (err & rtk::kErrStall) m += (m.empty() ? "" : "; ") + std::string(kStallMsg);
+    return m;
+}
+
+// Bound on one continuous hand-off wait of ring mode (rt_units.h), in wait_clock units.  A wave
+// waits for the unit holding the previous sample chunk of the same 64 pixels, traced meanwhile by
+// another wave; that unit's time is bounded by its 3072 samples' paths.  Through the BVH it is
+// milliseconds on any scene (the final scene: ~1 ms), and 40 s is the bound.  Scenes without a tree
+// (list walk: > 2^15 leaves, or RTZIG_KERNEL) cost ~n per ray segment: 70 000 spheres measured
+// ~100x the final scene's per-segment cost; the bound grows by 40 s per 2^16 spheres, up to
+// kStallMaxSec (2^24 spheres, the ABI's maximum: 10 000 s).
+uint32_t stall_bound(bool bvh, uint32_t n_spheres) {
+    uint64_t sec = rtk::kStallBaseSec;
+    if (!bvh) sec *= std::max<uint64_t>(1, ((uint64_t)n_spheres + 65535) / 65536);
+    sec = std::min<uint64_t>(sec, rtk::kStallMaxSec);
+    return (uint32_t)(sec * rtk::kStallUnitsPerSec);
+}
+
 hipError_t make_event(hipEvent_t* e, bool timed) {
     return timed ? hipEventCreate(e) : hipEventCreateWithFlags(e, hipEventDisableTiming);
 }
@@ -579,7 +628,6 @@ int rt_context_create(int device, rt_context** out_ctx) {
     if (e == hipSuccess) e = make_event(&ctx->done, false);
     int cus = 0;
     if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
-    ctx->ring_waves = (uint32_t)std::max(cus, 1) * kMaxWavesPerCU;
     ctx->sched_lanes = (uint64_t)std::max(cus, 1) * 16 * 64;
     if (e != hipSuccess) {
         const int rc = hip_fail(e, "rt_context_create: stream / event");
@@ -632,7 +680,7 @@ int rt_context_sync(rt_context* ctx) {
     if (err) {
         HIP_CHECK(hipMemsetAsync(ctx->d_ctr + rtk::kErrWord, 0, sizeof err, ctx->stream));
         HIP_CHECK(hipStreamSynchronize(ctx->stream));
-        rt_set_last_error(kStallMsg);
+        rt_set_last_error(err_message(err));
         return RT_ERR_HIP;
     }
     return RT_OK;
@@ -705,12 +753,37 @@ int rt_render_rows_async(rt_context* ctx, const rt_camera* cam, uint32_t output_
             direct = true;
         }
     }
+    const bool bvh = use_bvh(ctx);
+    rtk::KernelParams p = make_params(cam, row0, row_step, n_rows, ctx->n_spheres);
+    p.prof = ctx->profile && d_stats ? 1u : 0u;
+    p.s_begin = 0;
+    p.s_count = cam->samples_per_pixel;
+    // the launch for this call's kernel (plan_waves != nullptr: size the grid, launch nothing)
+    auto launch = [&](const rtk::UnitArgs* u, uint32_t* plan_waves) -> hipError_t {
+        if (bvh && ctx->precision == RT_PRECISION_F32)
+            return rtk_launch_samples_fast(&p, &ctx->bvh, ctx->d_geo, ctx->d_mat, u, d_stats, s, &ctx->last_kernel,
+                                           direct, plan_waves);
+        if (bvh)
+            return rtk_launch_samples_bvh(&p, &ctx->bvh, ctx->d_geo, ctx->d_mat, u, d_stats, s, &ctx->last_kernel,
+                                          direct, plan_waves);
+        return rtk_launch_samples(&p, ctx->d_geo, ctx->d_mat, u, d_stats, s, &ctx->last_kernel, direct, plan_waves);
+    };
+    // a context holds the workspace of one mode at a time (rt.h "Workspace")
     if (direct) {
-        rc = ensure_buffer(ctx, (void**)&ctx->d_samples, &ctx->samples_bytes, direct_bytes);
+        rc = release_buffer(ctx, (void**)&ctx->d_ring, &ctx->ring_bytes);
+        if (!rc) rc = release_buffer(ctx, (void**)&ctx->d_sums, &ctx->sums_bytes);
+        ctx->ring_waves = 0;
+        if (!rc) rc = fit_buffer(ctx, (void**)&ctx->d_samples, &ctx->samples_bytes, direct_bytes);
     } else {
-        rc = ensure_buffer(ctx, (void**)&ctx->d_ring, &ctx->ring_bytes,
-                           (size_t)ctx->ring_waves * rtk::kRingWaveDoubles * sizeof(double));
-        if (!rc && ua.n_chunks > 1) rc = ensure_buffer(ctx, (void**)&ctx->d_sums, &ctx->sums_bytes, P * 3 * sizeof(double));
+        // the ring holds the persistent grid of the kernel this call launches (its resident waves)
+        uint32_t waves = 0;
+        HIP_CHECK(launch(&ua, &waves));
+        waves = std::max(waves, 1u);
+        constexpr size_t kWaveBytes = rtk::kRingWaveDoubles * sizeof(double);
+        rc = release_buffer(ctx, (void**)&ctx->d_samples, &ctx->samples_bytes);
+        if (!rc) rc = fit_buffer(ctx, (void**)&ctx->d_ring, &ctx->ring_bytes, (size_t)waves * kWaveBytes);
+        ctx->ring_waves = rc ? 0u : (uint32_t)(ctx->ring_bytes / kWaveBytes);
+        if (!rc && ua.n_chunks > 1) rc = fit_buffer(ctx, (void**)&ctx->d_sums, &ctx->sums_bytes, P * 3 * sizeof(double));
     }
     const size_t flag_bytes = (n_tiles * sizeof(uint32_t) + 15) & ~(size_t)15;  // memset in 16-B multiples
     if (!rc) rc = ensure_buffer(ctx, (void**)&ctx->d_flags, &ctx->flags_bytes, flag_bytes);
@@ -737,12 +810,12 @@ int rt_render_rows_async(rt_context* ctx, const rt_camera* cam, uint32_t output_
     ua.P = (uint32_t)P;
     ua.out_format = output_format;
     ua.ring_waves = ctx->ring_waves;
+    ua.stall_ticks = stall_bound(bvh, ctx->n_spheres);
     // test hook RTZIG_STALL_US=<µs>: a shorter bound, so the tests can drive the give-up path (the
     // sticky error word, RT_ERR_HIP, and the next render succeeding)
-    ua.stall_ticks = rtk::kStallTicks;
     if (const char* e = std::getenv("RTZIG_STALL_US")) {
         const double us = std::atof(e);
-        if (us >= 0 && us * 100.0 < (double)rtk::kStallTicks) ua.stall_ticks = (uint32_t)(us * 100.0);
+        if (us >= 0 && us / rtk::kStallUnitUs < (double)ua.stall_ticks) ua.stall_ticks = (uint32_t)(us / rtk::kStallUnitUs);
     }
     ua.scale = cam->pixel_samples_scale;
 
@@ -761,19 +834,9 @@ int rt_render_rows_async(rt_context* ctx, const rt_camera* cam, uint32_t output_
     if (ctx->done_valid && ctx->done_stream != s) HIP_CHECK(hipStreamWaitEvent(s, ctx->done, 0));
     HIP_CHECK(hipMemsetAsync(ctx->d_ctr, 0, rtk::kCtrLaunchBytes, s));  // not the sticky error word
     if (!direct) HIP_CHECK(hipMemsetAsync(ctx->d_flags, 0, flag_bytes, s));
-    const bool bvh = use_bvh(ctx);
-    rtk::KernelParams p = make_params(cam, row0, row_step, n_rows, ctx->n_spheres);
-    p.prof = ctx->profile && d_stats ? 1u : 0u;
-    p.s_begin = 0;
-    p.s_count = cam->samples_per_pixel;
     hipEvent_t* ev = ctx->timing ? &ctx->events[3 * ctx->call_first] : nullptr;
     if (ev) HIP_CHECK(hipEventRecord(ev[0], s));
-    if (bvh && ctx->precision == RT_PRECISION_F32)
-        HIP_CHECK(rtk_launch_samples_fast(&p, &ctx->bvh, ctx->d_geo, ctx->d_mat, &ua, d_stats, s, &ctx->last_kernel));
-    else if (bvh)
-        HIP_CHECK(rtk_launch_samples_bvh(&p, &ctx->bvh, ctx->d_geo, ctx->d_mat, &ua, d_stats, s, &ctx->last_kernel));
-    else
-        HIP_CHECK(rtk_launch_samples(&p, ctx->d_geo, ctx->d_mat, &ua, d_stats, s, &ctx->last_kernel));
+    HIP_CHECK(launch(&ua, nullptr));
     if (ev) HIP_CHECK(hipEventRecord(ev[1], s));
     if (direct) HIP_CHECK(rtk_launch_reduce(&ua, s));
     if (ev) HIP_CHECK(hipEventRecord(ev[2], s));
@@ -840,6 +903,13 @@ int rt_context_kernel_times_total(rt_context* ctx, double* sample_ms, double* re
 }
 
 const char* rt_kernel_name(rt_context* ctx) { return ctx ? ctx->last_kernel : "render_kernel"; }
+
+int rt_context_workspace_bytes(rt_context* ctx, uint64_t* bytes) {
+    if (!ctx || !bytes) { rt_set_last_error("null context / output"); return RT_ERR_INVALID; }
+    *bytes = (uint64_t)ctx->ring_bytes + ctx->sums_bytes + ctx->flags_bytes + ctx->samples_bytes + ctx->sched_bytes +
+             (ctx->d_ctr ? rtk::kCtrBytes : 0);
+    return RT_OK;
+}
 
 }  // extern "C"
 
@@ -1013,7 +1083,7 @@ int rt_render(const rt_camera* cam, const rt_sphere* spheres, size_t n, const rt
             e = hipMemsetAsync(c->d_ctr + rtk::kErrWord, 0, sizeof(uint64_t), c->stream);
             if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
             rcs[g] = RT_ERR_HIP;
-            msgs[g] = kStallMsg;
+            msgs[g] = err_message(c->h_stats[2]);
             return;
         }
         st_rays[g] = c->h_stats[0];

@@ -1,6 +1,6 @@
 // rt_units.h — device side of the unit scheduler and the ordered in-kernel accumulation
-// (rt_kernel.h "Work units").  Shared by the parity kernels (rt_kernel.hip) and the
-// fast kernel (rt_kernel_fast.hip).
+// (rt_kernel.h "Work units").  Shared by every sample kernel of rt_kernel.hip (parity
+// list / BVH walks and the f32 fast mode, all instantiations of one path_loop).
 //
 // Hand-off between waves (possibly on different XCDs, whose L2s are not coherent with each other):
 // the running sums are stored write-through (sc1: agent-scope relaxed atomic stores), every storing
@@ -22,6 +22,22 @@ namespace rtk {
 typedef __attribute__((address_space(1))) unsigned long long gu64;
 typedef __attribute__((address_space(1))) uint32_t gu32;
 
+// Debug builds (-DRTZIG_BOUNDS=1, tools/diag_modes.py): every index into a global buffer or a lane's
+// LDS stack is checked; one out of range sets kErrBounds in the sticky error word (the host reports
+// it: rt_context_sync / rt_render) and the access is skipped or redirected in range, so a bad index
+// shows up as a reported error instead of a memory fault.  Shipped builds compile the checks away.
+#ifndef RTZIG_BOUNDS
+#define RTZIG_BOUNDS 0
+#endif
+constexpr bool kBounds = RTZIG_BOUNDS != 0;
+__device__ __forceinline__ bool bounds_ok(bool ok, unsigned long long* ctr) {
+    if constexpr (kBounds) {
+        if (!ok) atomicOr(ctr + kErrWord, kErrBounds);
+        return ok;
+    }
+    return true;
+}
+
 __device__ __forceinline__ double ld_wt(const double* p) {  // global_load_dwordx2 ... sc1
     return __builtin_bit_cast(double, __hip_atomic_load((gu64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
 }
@@ -34,13 +50,14 @@ __device__ __forceinline__ void st_wt(double* p, double v) {  // global_store_dw
 // (s_memrealtime, a constant 100 MHz), not by a count of sleeps: a predecessor unit may legitimately
 // take seconds to trace (a scene too large for the tree, walked linearly: ~100x the final scene's
 // per-ray cost at 70 000 spheres), and a fixed sleep count scaled with nothing.  The clock restarts
-// whenever this wave claims or finalises a unit; past kStallTicks the wave reports it in the
-// sticky ctr[kErrWord] and gives up (the host returns RT_ERR_HIP).  The wait's state is ONE SGPR,
-// as the round-2 sleep counter was: a global-progress bound (every finalisation counted, the count
-// and the clock carried by the waiting wave) cost 1.1-1.7% of the frame through SGPR spills into
-// the walk's VGPRs.  The clock is kept as its low 32 bits (wrapping differences are exact below
-// 2^32 ticks = 42.9 s).
-__device__ __forceinline__ uint64_t realtime() { return __builtin_amdgcn_s_memrealtime(); }
+// whenever this wave claims or finalises a unit; past ua.stall_ticks the wave reports it in the
+// sticky ctr[kErrWord] and gives up (the host returns RT_ERR_HIP).  The bound is set per launch by
+// the host (rt_runtime.cpp stall_bound: 40 s, scaled with the sphere count for list walks).  The
+// wait's state is ONE SGPR, as the round-2 sleep counter was: a global-progress bound (every
+// finalisation counted, the count and the clock carried by the waiting wave) cost 1.1-1.7% of the
+// frame through SGPR spills into the walk's VGPRs.  The clock is kept in units of 256 ticks
+// (kStallTickNs = 2.56 µs) as 32 bits: wrapping differences are exact below 2^32 units = 3.05 h.
+__device__ __forceinline__ uint32_t wait_clock() { return (uint32_t)(__builtin_amdgcn_s_memrealtime() >> 8); }
 
 
 // Wave-uniform scheduler state (every member is the same in all 64 lanes).  kDirect: direct mode
@@ -55,7 +72,7 @@ struct UnitSched {
     uint32_t cur_tile = 0, cur_s0 = 0;
     uint32_t st_u[kSlots];           // unit id held by each slot
     uint32_t spins = 0;              // sleeps in all (diagnostics)
-    uint32_t wait_t0 = 0;            // realtime (low word, | 1) when the current wait began (0: not waiting)
+    uint32_t wait_t0 = 0;            // wait_clock() | 1 when the current wait began (0: not waiting)
     uint32_t seen = 0;               // direct mode: item position after this wave's last claim
     uint32_t waves = 1;              // direct mode: the launch's waves
     uint32_t seg = 0, empty = 0;     // direct mode: segment claimed from; segments found empty
@@ -66,6 +83,9 @@ struct UnitSched {
     bool failed = false;             // stall bound reached (reported in ctr[kErrWord])
 
     __device__ UnitSched(const UnitArgs& a, uint32_t wave) : ua(a), ring(a.ring + (size_t)wave * kRingWaveDoubles) {
+        if constexpr (kBounds && !kDirect) {
+            if (!bounds_ok(wave < a.ring_waves, a.ctr)) ring = a.ring;
+        }
         if constexpr (kDirect) {
             waves = gridDim.x * (blockDim.x / 64);
             seg = blockIdx.x % kSegs;
@@ -182,6 +202,9 @@ struct UnitSched {
     // The color of a finished item goes to its unit's ring slot: [slot][m][3] (direct mode:
     // samples[m = s * P + q]).
     __device__ __forceinline__ void store(uint32_t slot, uint32_t m, double x, double y, double z) const {
+        if constexpr (kBounds) {
+            if (!bounds_ok(kDirect ? m < ua.n_units : slot < kSlots && m < kUnitS * 64, ua.ctr)) return;
+        }
         double* d = kDirect ? ua.samples + 3 * (size_t)m : ring + (size_t)slot * kRingSlotDoubles + 3 * m;
         d[0] = x;
         d[1] = y;
@@ -210,6 +233,12 @@ struct UnitSched {
 #pragma unroll
             for (uint32_t jj = 1; jj < kSlots; ++jj) u = jj == j ? st_u[jj] : u;
             const uint32_t k = fastdiv(u, ua.div_tiles), tile = u - k * ua.n_tiles;
+            if constexpr (kBounds) {
+                if (!bounds_ok(tile < ua.n_tiles && k < ua.n_chunks, ua.ctr)) {
+                    busy &= ~(1u << j);
+                    return true;
+                }
+            }
             uint32_t f = k;
             if (k) {  // chunk 0 has no predecessor
                 if (lane == 0) f = __hip_atomic_load((gu32*)ua.flags + tile, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -279,11 +308,11 @@ struct UnitSched {
     // Nothing to trace in this wave: wait for a dependency (bounded).  False: give up (reported).
     __device__ __forceinline__ bool wait(uint32_t lane) {
         ++spins;
-        const uint32_t now = (uint32_t)realtime() | 1u;
+        const uint32_t now = wait_clock() | 1u;
         if (wait_t0 == 0) {
             wait_t0 = now;
         } else if (now - wait_t0 > ua.stall_ticks) {
-            if (lane == 0) atomicOr(ua.ctr + kErrWord, 1ull);
+            if (lane == 0) atomicOr(ua.ctr + kErrWord, kErrStall);
             failed = true;
             return false;
         }

@@ -212,6 +212,12 @@ class DeviceRenderer:
     def kernel_name(self):
         return self.lib.rt_kernel_name(self.ctx).decode()
 
+    def workspace_bytes(self):
+        """Device bytes the context's render workspace holds (rt.h "Workspace")."""
+        b = C.c_uint64()
+        check("rt_context_workspace_bytes", self.lib.rt_context_workspace_bytes(self.ctx, C.byref(b)))
+        return b.value
+
     def enable_timing(self, enable=True):
         check("rt_context_enable_timing", self.lib.rt_context_enable_timing(self.ctx, int(enable)))
 

@@ -28,10 +28,12 @@ def assemble(gathered, height):
     return img[:height]
 
 
-def gather_image(local, height, rank, world, group=None):
+def gather_image(local, height, rank, world, group=None, collective=False):
     """local: (R, W, C) padded rows of this rank (rows beyond its n_rows are ignored).
-    Returns the (H, W, C) image on rank 0 and None elsewhere."""
-    if world == 1:
+    Returns the (H, W, C) image on rank 0 and None elsewhere.  At world 1 the rows are the image;
+    collective=True still runs the gather through the process group (bench.py --collective: the
+    RCCL path exercised on a 1-GPU box with a 1-rank nccl group)."""
+    if world == 1 and not collective:
         return local[:height]
     if rank == 0:
         # the peers' rows land in views of ONE (world, R, W, C) buffer: no stack copy

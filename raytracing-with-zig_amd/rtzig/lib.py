@@ -19,6 +19,7 @@ EXPORTED = [
     "rt_context_set_scene",
     "rt_render_rows_async",
     "rt_kernel_name",
+    "rt_context_workspace_bytes",
     "rt_context_enable_timing",
     "rt_context_kernel_times",
     "rt_context_kernel_times_total",
@@ -62,6 +63,7 @@ def _declare(lib):
         "rt_render_rows_async": (C.c_int, [vp, P(RtCamera), C.c_uint32, C.c_uint32, C.c_uint32,
                                            C.c_uint32, vp, vp, vp]),
         "rt_kernel_name": (C.c_char_p, [vp]),
+        "rt_context_workspace_bytes": (C.c_int, [vp, P(C.c_uint64)]),
         "rt_context_enable_timing": (C.c_int, [vp, C.c_int]),
         "rt_context_kernel_times": (C.c_int, [vp, P(C.c_double), P(C.c_double)]),
         "rt_context_kernel_times_total": (C.c_int, [vp, P(C.c_double), P(C.c_double), P(C.c_uint32)]),

@@ -115,3 +115,34 @@ def test_bench_refuses_what_it_cannot_run():
     if torch.cuda.device_count() < 2:
         rc, lines, err = _bench(["--gpus", "2", "--steps", "1", "--warmup", "0"])
         assert rc != 0 and lines == [] and "need 2 visible GPUs" in err
+
+
+def _one_rank_collective(port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=0, world_size=1)
+    try:
+        H = 5
+        local = torch.arange(H * 4 * 3, dtype=torch.float64).reshape(H, 4, 3)
+        img = rdist.gather_image(local, H, 0, 1, collective=True)
+        q.put((img.data_ptr() != local.data_ptr(), torch.equal(img, local)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_world1_collective_gather_goes_through_the_group():
+    """collective=True at world 1 (bench.py --collective): the rows travel through dist.gather on a
+    1-rank group (a new buffer), not the world-1 shortcut that returns the local rows."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_one_rank_collective, args=(_free_port(), q))
+    p.start()
+    copied, equal = q.get(timeout=120)
+    p.join(timeout=60)
+    assert p.exitcode == 0 and copied and equal
+
+
+def test_bench_collective_flag_forms_one_rank_group():
+    rc, lines, err = _bench(["--gpus", "1", "--collective", "--launch-check"])
+    assert rc == 0, err[-2000:]
+    assert lines == [{"launch_check": True, "n_gpus": 1, "gpus_arg": 1}]

@@ -100,3 +100,24 @@ def test_bench_pipelined_gather_bit_exact():
     line = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
     assert line["n_gpus"] == 2
     assert line["check"].startswith("gathered frame == whole-image render")
+
+
+def test_bench_rccl_gather_world1_bit_exact():
+    """The RCCL collective path on one MI355X: bench.py --collective joins a 1-rank nccl group and
+    runs the N>1 pipeline unchanged (two row buffers, render stream, dist.gather through
+    ProcessGroupNCCL on the collective stream each frame).  `--check`: rank 0's last gathered frame
+    equals a whole-image render bit for bit (reference: the row loop of camera.zig:128-140)."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    args = ["--gpus", "1", "--collective", "--dist-backend", "nccl", "--check", "--steps", "4", "--warmup", "1",
+            "--spp", "8", "--width", "240", "--no-cpu-baseline", "--no-fast", "--no-dropin"]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    p = subprocess.run([sys.executable, os.path.join(root, "bench.py")] + args, capture_output=True, text=True,
+                       timeout=110, cwd=root, env=env)
+    assert p.returncode == 0, p.stderr[-2000:]
+    line = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
+    assert line["n_gpus"] == 1
+    assert "RCCL gather to rank 0 (1-rank group" in line["config"]["parallelism"]
+    assert line["check"].startswith("gathered frame == whole-image render")

@@ -51,6 +51,9 @@ struct Segs {  // SoA of the recorded segments, replayed: segment j of the launc
     const double *ox, *oy, *oz, *dx, *dy, *dz;
     uint32_t n;       // recorded segments
     uint32_t total;   // segments traced by the launch (n x replays)
+    const uint32_t* path0;  // [n_paths + 1]: path p's segments are [path0[p], path0[p + 1]) (raster order)
+    uint32_t n_paths;       // recorded paths (one camera sample each)
+    uint32_t total_paths;   // paths traced by the launch (n_paths x replays)
 };
 
 // Static assignment: lane g of the grid (G lanes) traces segments g, g + G, g + 2G, ... (a shared
@@ -113,6 +116,82 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(kWaves, kWave
                     check += (uint64_t)(k + 1) + __builtin_bit_cast(uint64_t, t);
                 }
                 active = false;
+            }
+        }
+    }
+    for (int off = 32; off > 0; off >>= 1) check += __shfl_xor(check, off, 64);
+    if (lane == 0) atomicAdd(sum, (unsigned long long)check);
+}
+// Path-ordered variant (round 4): the lanes of a wave trace whole PATHS the way
+// the megakernel's lanes do — wave w owns a contiguous range of paths (raster order, so its lanes start
+// on neighbouring pixels' camera rays), a lane walks its path's segments one after another, and a
+// lane whose path has ended takes the wave's next path (ballot + mbcnt, no atomics).  Dynamic fetch as
+// in the product.  The static-stride kernel above gives neighbouring lanes consecutive segments of ONE
+// path (a camera ray next to its own bounces), which the megakernel never does.
+template <int B, class StackT, int kWaves>
+__global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(kWaves, kWaves))) void walk_kernel_paths(
+    KernelParams kp_unused, BvhArgs b, Segs sg, double t_min, int32_t* __restrict__ out_k,
+    double* __restrict__ out_t, unsigned long long* __restrict__ ctr, unsigned long long* __restrict__ sum) {
+    extern __shared__ __align__(16) unsigned char lds_raw[];
+    const size_t scene_bytes = (size_t)bvh_leaves_offset(b.n_nodes) + (size_t)b.n_leaves * sizeof(BvhLeaf);
+    StackT* stack = (StackT*)(lds_raw + scene_bytes);
+    using W = BvhWalker<true, B, StackT>;
+    stack[threadIdx.x] = (StackT)W::kEnd;
+    BvhNode* ln = (BvhNode*)lds_raw;
+    BvhLeaf* ll = (BvhLeaf*)(lds_raw + bvh_leaves_offset(b.n_nodes));
+    for (uint32_t k = threadIdx.x; k < b.n_nodes; k += blockDim.x) ln[k] = b.nodes[k];
+    for (uint32_t k = threadIdx.x; k < b.n_leaves; k += blockDim.x) ll[k] = b.leaves[k];
+    __syncthreads();
+    const W walk{ln, ll, b.always_geo, b.always_sid, b.n_always, stack + threadIdx.x, b.origin_bound, nullptr, 0};
+    const uint32_t lane = lane_id();
+    const uint32_t waves = gridDim.x * (blockDim.x / 64);
+    const uint32_t wave = blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
+    const uint32_t per = (sg.total_paths + waves - 1) / waves;
+    uint32_t pnext = wave * per;                                        // wave-uniform
+    const uint32_t pend = pnext + per < sg.total_paths ? pnext + per : sg.total_paths;
+    bool active = false, susp = false, has_path = false;
+    uint32_t seg = 0, seg_end = 0, rep = 0;  // the lane's current segment, its path's end, replay round
+    Ray r;
+    typename W::State ws;
+    Prof<false> pr;
+    uint64_t check = 0;
+    while (true) {
+        // lanes without a segment: the next segment of their path, or a new path from the wave's range
+        const uint64_t need = __ballot(!has_path);
+        if (need != 0 && pnext < pend) {
+            const uint32_t rk = rank_in(need);
+            if (!has_path && pnext + rk < pend) {
+                const uint32_t pg = pnext + rk, p = pg % sg.n_paths;
+                rep = pg / sg.n_paths;
+                seg = sg.path0[p];
+                seg_end = sg.path0[p + 1];
+                has_path = true;
+            }
+            const uint32_t got = (uint32_t)__popcll(need);
+            pnext = pnext + got < pend ? pnext + got : pend;
+        }
+        if (has_path && !active) {
+            r.orig = mk(sg.ox[seg], sg.oy[seg], sg.oz[seg]);
+            r.dir = mk(sg.dx[seg], sg.dy[seg], sg.dz[seg]);
+            active = true;
+            susp = false;
+        }
+        if (__ballot(active) == 0) break;
+        if (active) {
+            __builtin_amdgcn_s_setprio(2);
+            double t;
+            const int k = walk.template run<(kRefetchK > 0)>(r, t_min, __builtin_inf(), &t, pr, ws, susp);
+            __builtin_amdgcn_s_setprio(0);
+            susp = k == kSuspended;
+            if (!susp) {
+                if (rep == 0) {
+                    out_k[seg] = k;
+                    out_t[seg] = t;
+                } else {
+                    check += (uint64_t)(k + 1) + __builtin_bit_cast(uint64_t, t);
+                }
+                active = false;
+                if (++seg == seg_end) has_path = false;
             }
         }
     }
@@ -240,6 +319,16 @@ int main(int argc, char** argv) {
     // the replayed workload: a different sample of the same camera's paths
     const auto segs = rtbvh::sample_rays(sp.data(), n, cam, sah, n_samples, 0x0cc0ffee);
     const uint32_t ns = (uint32_t)segs.size();
+    // path boundaries: sample_rays records each path's segments consecutively, starting with its
+    // camera ray (origin within the defocus disk around the camera center)
+    std::vector<uint32_t> path0;
+    for (uint32_t i = 0; i < ns; i++) {
+        double d2 = 0;
+        for (int a = 0; a < 3; a++) d2 += (segs[i].o[a] - cam.center[a]) * (segs[i].o[a] - cam.center[a]);
+        if (d2 < 1.0) path0.push_back(i);  // the disk radius is 10 * tan(0.3 deg) = 0.052
+    }
+    path0.push_back(ns);
+    const uint32_t n_paths = (uint32_t)path0.size() - 1;
     std::vector<double> h[6];
     for (auto& v : h) v.reserve(ns);
     for (const auto& s : segs)
@@ -248,7 +337,8 @@ int main(int argc, char** argv) {
             h[3 + a].push_back(s.d[a]);
         }
     occ::Segs sg{upload(h[0]), upload(h[1]), upload(h[2]), upload(h[3]), upload(h[4]), upload(h[5]), ns,
-                 (uint32_t)std::min<uint64_t>((uint64_t)ns * replays, 0xffffffffull)};
+                 (uint32_t)std::min<uint64_t>((uint64_t)ns * replays, 0xffffffffull), upload(path0), n_paths,
+                 (uint32_t)std::min<uint64_t>((uint64_t)n_paths * replays, 0xffffffffull)};
     rtk::BvhArgs b{};
     b.nodes = upload(dt.nodes);
     b.leaves = upload(dt.leaves);
@@ -324,11 +414,21 @@ int main(int argc, char** argv) {
         std::fprintf(stderr, "%-12s B=%4d blocks/CU=%d waves/SIMD=%d  %.3f ms  %.4f ns/segment\n", name, B, per_cu,
                      per_cu * B / 256, med, med * 1e6 / sg.total);
     };
-    run(occ::walk_kernel<512, int32_t, 4>, "w4_i32", 512, 4, 4);
-    run(occ::walk_kernel<512, int16_t, 4>, "w4_i16", 512, 4, 2);
-    run(occ::walk_kernel<640, int16_t, 5>, "w5_i16", 640, 5, 2);
-    run(occ::walk_kernel<768, int16_t, 6>, "w6_i16", 768, 6, 2);
-    run(occ::walk_kernel<1024, int16_t, 8>, "w8_i16", 1024, 8, 2);
+    const char* mode = std::getenv("WALK_OCC_MODE");  // "stride" (round 3), "paths" (round 4), default both
+    if (!mode || std::strcmp(mode, "paths") != 0) {
+        run(occ::walk_kernel<512, int32_t, 4>, "w4_i32", 512, 4, 4);
+        run(occ::walk_kernel<512, int16_t, 4>, "w4_i16", 512, 4, 2);
+        run(occ::walk_kernel<640, int16_t, 5>, "w5_i16", 640, 5, 2);
+        run(occ::walk_kernel<768, int16_t, 6>, "w6_i16", 768, 6, 2);
+        run(occ::walk_kernel<1024, int16_t, 8>, "w8_i16", 1024, 8, 2);
+    }
+    if (!mode || std::strcmp(mode, "stride") != 0) {
+        run(occ::walk_kernel_paths<512, int32_t, 4>, "paths_w4_i32", 512, 4, 4);
+        run(occ::walk_kernel_paths<512, int16_t, 4>, "paths_w4_i16", 512, 4, 2);
+        run(occ::walk_kernel_paths<640, int16_t, 5>, "paths_w5_i16", 640, 5, 2);
+        run(occ::walk_kernel_paths<768, int16_t, 6>, "paths_w6_i16", 768, 6, 2);
+        run(occ::walk_kernel_paths<1024, int16_t, 8>, "paths_w8_i16", 1024, 8, 2);
+    }
 
     // host check of a sample against the reference's linear scan
     uint32_t checked = 0, mism = 0;
@@ -337,9 +437,9 @@ int main(int argc, char** argv) {
         const int k = scan(sp, segs[i].o, segs[i].d, 1e-3, &t);
         if (k != ref_k[i] || (k >= 0 && std::memcmp(&t, &ref_t[i], sizeof t) != 0)) mism++;
     }
-    std::printf("{\"segments_per_launch\": %u, \"recorded_segments\": %u, \"samples\": %zu, \"refetch_k\": %d, \"variants_bit_identical\": %s, "
+    std::printf("{\"segments_per_launch\": %u, \"recorded_segments\": %u, \"recorded_paths\": %u, \"samples\": %zu, \"refetch_k\": %d, \"variants_bit_identical\": %s, "
                 "\"host_scan_checked\": %u, \"host_scan_mismatches\": %u, \"results\": [",
-                sg.total, ns, n_samples, rtk::kRefetchK, all_equal ? "true" : "false", checked, mism);
+                sg.total, ns, n_paths, n_samples, rtk::kRefetchK, all_equal ? "true" : "false", checked, mism);
     for (size_t i = 0; i < res.size(); i++)
         std::printf("%s{\"variant\": \"%s\", \"block\": %d, \"blocks_per_cu\": %u, \"waves_per_simd\": %d, "
                     "\"stack_entry_bytes\": %d, \"ms\": %.4f, \"ns_per_segment\": %.4f}",
