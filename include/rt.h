@@ -181,8 +181,10 @@ int rt_context_kernel_times_total(rt_context* ctx, double* sample_ms, double* re
  * [17] idle sleeps of waves waiting on a hand-off, [18] deferred unit finalisations (previous chunk
  * of the tile not yet finalised), [19] refills that found no free ring slot, [20] / [21] sum / max over
  * waves of (wave end - the wave's first empty claim), [22] the last wave's first empty claim, [23..25]
- * the parts of [4]: wave-cycles finalising units, handing out items (claims), seeding + getRay; 0...}.  Counts 0-3 are
- * exact and deterministic; the cycles and wave-iteration counts are diagnostics. */
+ * the parts of [4]: wave-cycles finalising units, handing out items (claims), seeding + getRay;
+ * [26..31] wave-level executions: loop iterations, rejection trips, seeding blocks, walks started
+ * (always-list tests), shading blocks, unit finalisations}.  Counts 0-3 are exact and deterministic;
+ * the cycles and wave-level counts are diagnostics. */
 int rt_context_enable_profile(rt_context* ctx, int enable);
 
 /* ---- host mirror of the reference's Scene / CameraBuilder / Color / PPM ---------------------- */

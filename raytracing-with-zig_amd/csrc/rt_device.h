@@ -11,6 +11,19 @@
 
 #pragma clang fp contract(off)
 
+// Region markers (tools/region_table.py): -DRTZIG_MARKS=1 builds emit an assembly comment ";@R <name>"
+// where each region of the path loop starts (and "rare" on the slow paths behind wave-uniform
+// tests), so the per-region instruction table can attribute the kernel's basic blocks.  Shipped
+// builds emit nothing.
+#ifndef RTZIG_MARKS
+#define RTZIG_MARKS 0
+#endif
+#if RTZIG_MARKS
+#define RTK_MARK(x) asm volatile(";@R " x)
+#else
+#define RTK_MARK(x) ((void)0)
+#endif
+
 namespace rtk {
 
 // ------------------------------------------------------------------------------------------------
@@ -80,6 +93,7 @@ struct RayDiv {
         // scalar unit; folding it into the per-lane bool made the compiler materialize that bool
         // with two VALU ops per division.
         if (__builtin_expect((__ballot(far) | bad) != 0, 0)) {
+            RTK_MARK("rare");
             if (far || ((bad >> lane()) & 1)) q = x / a;
         }
         return q;
@@ -100,6 +114,7 @@ __device__ __forceinline__ double sqrt_g(double x) {
     double r = sqrt_normal(x);
     const bool slow = !sqrt_in_range(x);
     if (__builtin_expect(__ballot(slow) != 0, 0)) {
+        RTK_MARK("rare");
         if (slow) r = __builtin_sqrt(x);
     }
     return r;
@@ -116,6 +131,7 @@ __device__ __forceinline__ v3 unit(v3 a) {
     double inv = __builtin_fma(__builtin_fma(-len, y, 1.0), y, y);
     const bool slow = !sqrt_in_range(ls);
     if (__builtin_expect(__ballot(slow) != 0, 0)) {  // rare: wave-uniform test, see sqrt_g
+        RTK_MARK("rare");
         if (slow) inv = 1.0 / __builtin_sqrt(ls);
     }
     return muls(a, inv);
@@ -233,6 +249,7 @@ struct Rng {
         // the rare lanes are redone, behind a wave-uniform test so the common case has no
         // exec-mask branch
         if (__builtin_expect(__ballot(hi < (1u << 20)) != 0, 0)) {
+            RTK_MARK("rare");
             if (hi < (1u << 20)) res = uniform_slow(rnd);
         }
         return res;

@@ -5,25 +5,23 @@
 //     -> HittableList.hit (hittable.zig:64-77) -> Sphere.hit (sphere.zig:26-54)
 //     -> Material.scatter (material.zig:145-151)
 //
-// Two kernels (DESIGN.md "Kernels"):
+// One persistent launch per frame, plus a reduce pass in direct mode:
 //
-// sample_kernel — persistent waves pull work items (one item = one sample of one pixel) from a
-//   global queue (8 segments with a counter each, up to 2048 items per wave per atomic).  A lane
-//   whose path ends (miss / absorb / bounceMax) stores the sample's color and immediately takes
-//   the next item, so every lane of
-//   every wave traces one ray segment per loop iteration until the queue drains: no lane idles
-//   behind a long glass path and no CU idles behind a slow block.
-//   Sphere geometry {cx, cy, cz, r^2} is staged once per workgroup into LDS (32 B per sphere);
-//   every lane walks the list in order and all lanes of a wave read the same sphere (LDS
-//   broadcast, conflict-free).  Materials are read from global memory for the hit sphere only.
-//   The closest-hit scan keeps the reference's acceptance rule (strict surrounds on the shrinking
-//   interval) and computes the hit record for the winner only — the same bits as the reference's
-//   per-accepted-sphere record.
+// sample_kernel_bvh (parity, default), sample_kernel (the reference's linear list walk, tiny scenes)
+//   and sample_kernel_fast (RT_PRECISION_F32) all run path_loop below: persistent waves take work
+//   items (one item = one sample of one pixel) from the unit scheduler of rt_units.h; every lane
+//   traces one ray segment per loop iteration (rayColor's loop body), and a lane whose path ends
+//   (miss / absorb / bounceMax) stores the sample's colour and takes the next item, so no lane idles
+//   behind a long glass path and no CU idles behind a slow block.  Ring mode (large launches)
+//   accumulates each pixel's samples in sample order inside the kernel (wave rings + running sums
+//   handed from wave to wave); direct mode (small launches) stores every sample for the reduce pass.
+//   The closest hit is HittableList.hit's first-wins argmin, found by a BVH walk over an LDS-resident
+//   tree (BvhWalker) or the reference's list walk (LinearWalker) with the same f64 quadratic.
 //
-// reduce_kernel — per pixel, adds the stored sample colors in sample order to a running f64 sum
-//   (camera.zig:135 `pixelColor += rayColor(ray)` — the same sequence of roundings as the
-//   reference's loop), then scales by pixelSamplesScale (camera.zig:137) and writes linear f64 or
-//   the fused Color.toRgb bytes (color.zig:63-80).
+// reduce_kernel — direct mode only: per pixel, adds the stored sample colours in sample order
+//   (camera.zig:135 `pixelColor += rayColor(ray)`, the same sequence of roundings as the reference's
+//   loop), then scales by pixelSamplesScale (camera.zig:137) and writes linear f64 or the fused
+//   Color.toRgb bytes (color.zig:63-80).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -337,6 +335,14 @@ struct LinearWalker {
 // v_max/v_min.  With IEEE mode on (the default) these return the non-NaN operand for quiet NaNs —
 // exactly fmaxf/fminf on every value this walk produces (arithmetic never yields signaling NaNs) —
 // but written as builtins the compiler re-canonicalizes the loop-carried bounds every iteration.
+#if RTZIG_WALK_FORM >= 1
+__device__ __forceinline__ float slab_near(float x, float y, float z, float lower) {
+    return __builtin_fmaxf(__builtin_fmaxf(x, y), __builtin_fmaxf(z, lower));
+}
+__device__ __forceinline__ float slab_far(float x, float y, float z, float upper) {
+    return __builtin_fminf(__builtin_fminf(x, y), __builtin_fminf(z, upper));
+}
+#else
 __device__ __forceinline__ float slab_near(float x, float y, float z, float lower) {
     float t, r;
     asm volatile("v_max_f32 %0, %1, %2" : "=v"(t) : "v"(z), "v"(lower));
@@ -349,6 +355,7 @@ __device__ __forceinline__ float slab_far(float x, float y, float z, float upper
     asm volatile("v_min3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(x), "v"(y), "v"(t));
     return r;
 }
+#endif
 
 // v_cndmask_b32 on a wave mask held in SGPRs: lanes whose bit of `m` is set get `t`, others `f`
 __device__ __forceinline__ int32_t sel_mask(int32_t f, int32_t t, uint64_t m) {
@@ -374,10 +381,18 @@ constexpr int kSuspended = -2;
 typedef float f2 __attribute__((ext_vector_type(2)));
 // {b.x * m.x + a.x, b.y * m.x + a.x}: v_pk_fma_f32 with the second and third operands' low halves
 // broadcast to the high lane (op_sel_hi:[1,0,0]); their high halves are never read
+#ifndef RTZIG_WALK_FORM
+#define RTZIG_WALK_FORM 0
+#endif
 __device__ __forceinline__ f2 pk_fma_lo(f2 b, f2 m, f2 a) {
+#if RTZIG_WALK_FORM >= 1
+    const f2 mm = {m.x, m.x}, aa = {a.x, a.x};
+    return __builtin_elementwise_fma(b, mm, aa);
+#else
     f2 r;
     asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[1,0,0]" : "=v"(r) : "v"(b), "v"(m), "v"(a));
     return r;
+#endif
 }
 typedef int32_t i2 __attribute__((ext_vector_type(2)));
 
@@ -659,7 +674,7 @@ struct BvhWalker {
             pr.inner_iter();
             f2 bx0, by0, bz0, bx1, by1, bz1;
             int32_t ref0, ref1, popped;
-            if constexpr (kLdsNodes) {
+            if constexpr (kLdsNodes && RTZIG_WALK_FORM < 2) {
                 // nodes start at LDS address 0: the ref is the address.  Seven ds_read_b64
                 // (2 LDS cycles each); left to itself the compiler pairs them into
                 // ds_read2_b64 (8 cycles for the same 16 B) behind extra base adds.
@@ -675,6 +690,22 @@ struct BvhWalker {
                                "+v"(popped));
                 ref0 = refs.x;
                 ref1 = refs.y;
+            } else if constexpr (kLdsNodes) {
+                // the same reads as plain LDS loads (form 2): the compiler pairs each axis's two planes
+                // into one ds_read2_b64 and waits for them one by one.  Nodes start at LDS address 0, so
+                // the ref is the address itself.
+                typedef const __attribute__((address_space(3))) char* lds_cp;
+                const lds_cp nb = (lds_cp)(uintptr_t)(uint32_t)cur;
+                bx0 = *(const __attribute__((address_space(3))) f2*)(nb + ax);
+                by0 = *(const __attribute__((address_space(3))) f2*)(nb + ay);
+                bz0 = *(const __attribute__((address_space(3))) f2*)(nb + az);
+                bx1 = *(const __attribute__((address_space(3))) f2*)(nb + 48 + ax);
+                by1 = *(const __attribute__((address_space(3))) f2*)(nb + 48 + ay);
+                bz1 = *(const __attribute__((address_space(3))) f2*)(nb + 48 + az);
+                const i2 refs = *(const __attribute__((address_space(3))) i2*)(nb + 96);
+                ref0 = refs.x;
+                ref1 = refs.y;
+                popped = *top;
             } else {
                 const char* nb = (const char*)nodes + cur;  // byte-offset ref
                 bx0 = *(const f2*)(nb + ax); by0 = *(const f2*)(nb + ay); bz0 = *(const f2*)(nb + az);
@@ -696,6 +727,14 @@ struct BvhWalker {
             // The three compares are taken as wave masks and combined on the scalar unit, and
             // the selects are v_cndmask on those masks: 3 compares + 5 selects (the compiler's
             // form of the same logic re-compared a negated mask on the VALU).
+#if RTZIG_WALK_FORM >= 3
+            const bool h0 = n0 <= f0, h1 = n1 <= f1, nf = n0 <= n1;
+            const bool p0 = h0 && (!h1 || nf);
+            const int32_t near = p0 ? ref0 : ref1, far = p0 ? ref1 : ref0;
+            top[kStride] = (StackT)far;
+            cur = (h0 || h1) ? near : popped;
+            top += (h0 && h1) ? kStride : ((h0 || h1) ? 0 : -kStride);
+#else
             const uint64_t m0 = __ballot(n0 <= f0), m1 = __ballot(n1 <= f1), mf = __ballot(n0 <= n1);
             const uint64_t pick0 = m0 & (~m1 | mf);  // both: nearer; one: that one
             const uint64_t any = m0 | m1, both = m0 & m1;
@@ -703,6 +742,7 @@ struct BvhWalker {
             top[kStride] = (StackT)far;
             cur = sel_mask(popped, near, any);
             top += sel_mask(sel_mask(-kStride, 0, any), kStride, both);
+#endif
         }
     }
 
@@ -847,6 +887,7 @@ struct BvhWalker {
                              origin_bound;
         if (__builtin_expect(__ballot(far) != 0, 0)) {
             if (far) {
+                RTK_MARK("rare");
                 double t;
                 const int k = world_hit<1>(geo_all, n_pad, r, t_min, t_max, &t);
                 pr.tests(n_pad);
@@ -878,9 +919,11 @@ struct BvhWalker {
         // while-while (Aila & Laine 2009): every lane advances through internal nodes until it
         // holds a leaf (or is done); then the lanes with a leaf test its spheres together, so the
         // f64 leaf work runs with most lanes active instead of whenever any one lane hits a leaf.
+        RTK_MARK("walk_inner");
         while (cur != kEnd) {
             descend(cur, top, ax, ay, az, inv_x, inv_y, inv_z, noi_x, noi_y, noi_z, lower, upper, pr);
             if (cur != kEnd && !leaf_ok(cur)) cur = kEnd;
+            RTK_MARK("leaf");
             if (cur != kEnd) {
                 pr.leaf_iter();
                 // leaf: exactly kLeafBvh slots (sentinel-padded); the kLeafBvh discriminant chains
@@ -1110,6 +1153,10 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
     Prof<kProf> pr;
     uint64_t cyc_refill = 0, cyc_walk = 0, cyc_shade = 0, cyc_trips = 0;  // wave-uniform (kProf only)
     uint64_t cyc_fin = 0, cyc_hand = 0, cyc_seed = 0;  // parts of cyc_refill: finalise, hand-out, seed + getRay
+    // wave-level executions (kProf only; scalar, wave-uniform): loop iterations, trip-loop trips, seeding
+    // blocks, walks started (always-list tests), shading blocks, finalisations — with the per-step counts
+    // of Prof they weight the static instruction counts of each region (tools/region_table.py)
+    uint32_t n_iter = 0, n_trip = 0, n_seed = 0, n_wstart = 0, n_shade = 0, n_fin = 0;
     uint64_t rt_start = 0, rt_drain = 0;  // s_memrealtime (100 MHz) at start / first empty claim (kProf only)
     if constexpr (kProf) rt_start = __builtin_amdgcn_s_memrealtime();
 
@@ -1117,8 +1164,13 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
         uint64_t t_top = 0;
         if constexpr (kProf) t_top = __builtin_amdgcn_s_memtime();
         // ---- finalise one unit whose samples have all ended (rt_units.h) --------------------------
+        RTK_MARK("finalise");
         __builtin_amdgcn_s_setprio(2);  // the hand-off's dependent loads (see the walk below)
         const bool progressed = us.finalize_one(us.ready_mask(active, myslot), lane);
+        if constexpr (kProf) {
+            ++n_iter;
+            n_fin += progressed ? 1u : 0u;
+        }
         __builtin_amdgcn_s_setprio(0);
         uint64_t t_fin = 0;
         if constexpr (kProf) {
@@ -1126,6 +1178,7 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
             cyc_fin += t_fin - t_top;
         }
         // ---- hand new items to lanes without a path (wave-uniform control flow) ----------------
+        RTK_MARK("handout");
         bool fresh = false;
         uint32_t fq = 0, fs = 0;  // pixel (launch-local) and sample of a freshly handed item
         const bool was_drained = us.drained;
@@ -1138,6 +1191,8 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
         }
         // the lanes handed an item above start their path: seeding and getRay run once, outside
         // the claim loop, so the generator state and ray are not loop-carried through it
+        if constexpr (kProf) n_seed += __ballot(fresh) != 0 ? 1u : 0u;
+        RTK_MARK("seed");
         if (fresh) {
             const uint32_t row_local = fastdiv(fq, p.div_width);
             const uint32_t i = fq - row_local * W;
@@ -1149,6 +1204,7 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
             bounce = 0;
         }
         if constexpr (kProf) cyc_seed += __builtin_amdgcn_s_memtime() - t_ref;
+        RTK_MARK("idle");
         const bool idle = __ballot(active) == 0;
         if (idle) {
             // nothing to trace: finish (no unit left, none held), or claim again next iteration
@@ -1166,6 +1222,7 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
         }
 
         // ---- rejection loops, at most kRuvTrips trips per iteration ------------------------------
+        RTK_MARK("trips");
         // Two rejection samplers draw from a lane's stream: Vec.randomUnitVec (vec.zig:71-80) for a
         // pending Lambertian / Metal scatter (3 draws a trip, mean 1.91 trips) and randomInUnitDisk
         // (vec.zig:82-92) for a new camera ray's defocus sample (2 draws a trip, mean 1.27 trips).
@@ -1182,6 +1239,7 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
             const bool wr = pending && !got, wd = dpend && !dgot;
             const uint64_t need = __ballot(wr || wd);
             if (need == 0) break;
+            if constexpr (kProf) ++n_trip;
             if constexpr (kF32) {
                 if (wr || wd) trip_f32(g, wr, ux, uy, uz, uls, got, dgot);
             } else if (wr || wd) {
@@ -1197,6 +1255,7 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
                 }
             }
         }
+        RTK_MARK("scatter_finish");
         if (dgot) {
             camera_finish(ux, uy, r);
             dpend = false;
@@ -1225,11 +1284,17 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
             }
         }
         // ---- trace one ray segment per ready lane (rayColor's loop body, camera.zig:153-177) ---
+        RTK_MARK("walk_setup");
         // Lambertian and Metal scatters draw their randomUnitVec in the next iteration's trip loop
         if constexpr (kProf) {  // the trip loop counts as shading
             const uint64_t t = __builtin_amdgcn_s_memtime();
             cyc_trips += t - t_walk0;
             t_walk0 = t;
+        }
+        bool shaded = false;  // kProf: this lane ran the shading below
+        if constexpr (kProf) {
+            const bool walks = active && !done && !pending && !dpend && bounce < p.bounce_max;
+            n_wstart += __ballot(walks && !susp) != 0 ? 1u : 0u;
         }
         if (active && !done && !pending && !dpend) {
             if (bounce >= p.bounce_max) {
@@ -1253,10 +1318,14 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
                     k = walk(r, (Real)p.t_min, (Real)p.t_max, &t, pr);
                 }
                 __builtin_amdgcn_s_setprio(1);
+                RTK_MARK("shade");
                 if constexpr (kProf) {
                     if (bounce == 0) { pr.cam_visits += pr.n_visits - v0; pr.cam_tests += pr.n_tests - t0; }
                 }
-                if constexpr (kProf) t_walk1 = __builtin_amdgcn_s_memtime();
+                if constexpr (kProf) {
+                    t_walk1 = __builtin_amdgcn_s_memtime();
+                    shaded = !susp;
+                }
                 if constexpr (kF32) {
                     if (k >= 0 && !bounds_ok((uint32_t)k < p.n_spheres, ua.ctr)) k = -1;
                     if (!susp) shade_f32(k, t, geo_orig, mat_g, g, r, att, col, done, pending, sc_metal, sc_fuzz, sc_nrm,
@@ -1329,6 +1398,8 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
             }
         }
         __builtin_amdgcn_s_setprio(0);
+        if constexpr (kProf) n_shade += __ballot(shaded) != 0 ? 1u : 0u;
+        RTK_MARK("store");
         if (done) {
             us.store(myslot, mi, col.x, col.y, col.z);
             ++nsamples;
@@ -1352,6 +1423,7 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
         }
     }
 
+    RTK_MARK("epilogue");
     if (stats) {
         // wave-level reduction, one atomic pair per wave (all lanes converged here)
         for (int off = 32; off > 0; off >>= 1) {
@@ -1412,6 +1484,12 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
                 atomicAdd(&stats[23], (unsigned long long)cyc_fin);        // parts of stats[4]
                 atomicAdd(&stats[24], (unsigned long long)cyc_hand);
                 atomicAdd(&stats[25], (unsigned long long)cyc_seed);
+                atomicAdd(&stats[26], (unsigned long long)n_iter);
+                atomicAdd(&stats[27], (unsigned long long)n_trip);
+                atomicAdd(&stats[28], (unsigned long long)n_seed);
+                atomicAdd(&stats[29], (unsigned long long)n_wstart);
+                atomicAdd(&stats[30], (unsigned long long)n_shade);
+                atomicAdd(&stats[31], (unsigned long long)n_fin);
             }
         }
     }
@@ -1485,10 +1563,11 @@ __global__ __launch_bounds__(kBlockBvh) RTK_BVH_WAVES void sample_kernel_bvh(Ker
                                                                unsigned long long* __restrict__ stats) {
     RTK_BVH_BODY(false)
 }
-// Fast mode (RT_PRECISION_F32): the same body in f32; held to the parity kernel's 4 waves per SIMD
-// (left alone its ring-mode instantiation takes 131 VGPRs, i.e. 3 waves)
+// Fast mode (RT_PRECISION_F32): the same body in f32, under the same wave bound as the parity kernel
+// (4 waves per SIMD; left alone its ring-mode instantiation takes 131 VGPRs, i.e. 3 waves; the
+// instrumented builds 3, as for the parity kernel; RTZIG_BVH_WAVES overrides both)
 template <bool kLdsScene, bool kProf, bool kDirect>
-__global__ __launch_bounds__(kBlockBvh) __attribute__((amdgpu_waves_per_eu(4))) void sample_kernel_fast(
+__global__ __launch_bounds__(kBlockBvh) RTK_BVH_WAVES void sample_kernel_fast(
     KernelParams p, BvhArgs b, const GeoRec* __restrict__ geo_g, const MatRec* __restrict__ mat_g, UnitArgs ua,
     unsigned long long* __restrict__ stats) {
     RTK_BVH_BODY(true)

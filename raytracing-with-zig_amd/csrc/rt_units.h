@@ -258,6 +258,7 @@ struct UnitSched {
             // clobber keep every load below this point.
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             asm volatile("" ::: "memory");
+            RTK_MARK("fin_work");
             uint32_t s0, n;
             chunk_range(ua, k, &s0, &n);
             const uint32_t q = tile * 64 + lane;

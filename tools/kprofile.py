@@ -80,6 +80,14 @@ for v in args.variants.split():
                         "refill_parts": {"finalise": round(s[23] / cyc, 4), "hand_out": round(s[24] / cyc, 4),
                                          "seed_and_getRay": round(s[25] / cyc, 4)}},
         "scheduler": {"idle_sleeps": s[17], "deferred_finalisations": s[18], "refills_without_free_slot": s[19]},
+        # true wave-level executions per loop iteration (stats[26..31]; the *_per_wave_iter figures above
+        # are per 64 rays)
+        "wave_level": ({"iterations": s[26], "rays_per_iter": round(s[0] / s[26], 3),
+                        "inner_steps_per_iter": round(s[7] / s[26], 3), "leaf_rounds_per_iter": round(s[8] / s[26], 3),
+                        "cand_blocks_per_iter": round(s[9] / s[26], 3), "root2_blocks_per_iter": round(s[10] / s[26], 3),
+                        "trips_per_iter": round(s[27] / s[26], 3), "seed_blocks_per_iter": round(s[28] / s[26], 3),
+                        "walk_starts_per_iter": round(s[29] / s[26], 3), "shade_blocks_per_iter": round(s[30] / s[26], 3),
+                        "finalisations": s[31], "samples_per_iter": round(s[1] / s[26], 3)} if s[26] else None),
         "raw": s,
     }
     r.enable_profile(False)

@@ -64,9 +64,11 @@ def main(tag, workload):
             disp.setdefault(c, set()).add(r["Dispatch_Id"])
             key = (c, r["Dispatch_Id"])
             dur[key] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9
-            # rocprofv3's register fields as reported (VGPR_Count is not the compiler's count: the
-            # kernel compiles to 115 VGPRs, -Rpass-analysis=kernel-resource-usage, 4 waves / SIMD)
-            out["rocprof_VGPR_Count_field"], out["rocprof_SGPR_Count_field"] = int(r["VGPR_Count"]), int(r["SGPR_Count"])
+            # rocprofv3's register columns as it reports them; VGPR_Count is NOT the allocation (64
+            # for the 127-VGPR parity kernel): the compiler's figures are in kernel_resources.json
+            # (tools/kernel_resources.py), copied below as "compiler_resources"
+            out["rocprofv3_VGPR_Count_column (not the allocation)"] = int(r["VGPR_Count"])
+            out["rocprofv3_SGPR_Count_column"] = int(r["SGPR_Count"])
     kt = lambda c: sum(v for (cc, _), v in dur.items() if cc == c)  # kernel seconds under counter c's pass
     g = lambda c: sums.get(c, float("nan"))
     out["launches_per_frame"] = len(disp.get("SQ_WAVES", disp.get("FETCH_SIZE", ())))
@@ -100,6 +102,11 @@ def main(tag, workload):
         if "SQ_LDS_IDX_ACTIVE" in sums:
             out["lds"] = {"active_frac_of_cu_cycles": g("SQ_LDS_IDX_ACTIVE") / (256 * clock * T),
                           "bank_conflict_frac_of_active": g("SQ_LDS_BANK_CONFLICT") / g("SQ_LDS_IDX_ACTIVE")}
+    kr = os.path.join(dst, "kernel_resources.json")
+    if os.path.exists(kr) and "trace" in out:
+        mangled = {k: v for k, v in json.load(open(kr))["kernels"].items() if "sample_kernel_bvhILb1ELb0ELb0E" in k}
+        if mangled:
+            out["compiler_resources"] = next(iter(mangled.values()))
     json.dump(out, open(os.path.join(dst, "summary.json"), "w"), indent=1)
     if "hbm_bytes_per_frame" in out:
         keep = {k: out[k] for k in ("workload", "tag", "launches_per_frame", "hbm_bytes_per_frame", "fetch_bytes_per_frame",
