@@ -326,7 +326,8 @@ struct LinearWalker {
         return world_hit<U>(geo, n_pad, r, t_min, t_max, t);
     }
     template <bool kSusp, class PR>
-    __device__ __forceinline__ int run(const Ray& r, double t_min, double t_max, double* t, PR& pr, State&, bool) const {
+    __device__ __forceinline__ int run(const Ray& r, double t_min, double t_max, double* t, PR& pr, State&, bool,
+                                       bool = true) const {
         return (*this)(r, t_min, t_max, t, pr);
     }
 };
@@ -377,6 +378,14 @@ constexpr int32_t kDone = INT32_MIN;  // walk finished (stack entry 0)
 #define RTZIG_REFETCH_K 56
 #endif
 constexpr int kRefetchK = RTZIG_REFETCH_K;
+// Drain mode (RTZIG_DRAIN, default 1): once a wave's claims find the launch's items exhausted, its
+// walks stop suspending for refills (nothing is left to fetch) and its rejection loops run until
+// every lane has its sample instead of kRuvTrips trips per iteration, so the paths still in flight
+// at the end of a launch take fewer loop iterations (the drain tail).  Results unchanged.
+#ifndef RTZIG_DRAIN
+#define RTZIG_DRAIN 1
+#endif
+constexpr bool kDrainMode = RTZIG_DRAIN != 0;
 constexpr int kSuspended = -2;
 typedef float f2 __attribute__((ext_vector_type(2)));
 // {b.x * m.x + a.x, b.y * m.x + a.x}: v_pk_fma_f32 with the second and third operands' low halves
@@ -652,13 +661,15 @@ struct BvhWalker {
         State s;
         return run<false>(r, t_min, t_max, t_hit, pr, s, false);
     }
+    // refetch (wave-uniform): suspend walks for a shading batch (dynamic fetch); false once the
+    // launch's items are all handed out — there is nothing left to fetch, so walks run to the end
     template <bool kSusp, class PR>
     __device__ __forceinline__ int run(const RayT& r, Real t_min, Real t_max, Real* t_hit, PR& pr, State& st,
-                                       const bool resume) const {
+                                       const bool resume, const bool refetch = true) const {
         if constexpr (kF32) {
-            return run_f32<kSusp>(r, t_min, t_max, t_hit, pr, st, resume);
+            return run_f32<kSusp>(r, t_min, t_max, t_hit, pr, st, resume, refetch);
         } else {
-            return run_f64<kSusp>(r, t_min, t_max, t_hit, pr, st, resume);
+            return run_f64<kSusp>(r, t_min, t_max, t_hit, pr, st, resume, refetch);
         }
     }
 
@@ -748,7 +759,7 @@ struct BvhWalker {
 
     template <bool kSusp, class PR>
     __device__ __forceinline__ int run_f32(const fm::Ray& r, float t_min, float t_max, float* t_hit, PR& pr, State& st,
-                                           const bool resume) const {
+                                           const bool resume, const bool refetch) const {
         const float a = fm::len_sq(r.dir);
         const float inv_a = __builtin_amdgcn_rcpf(a);
         float closest = t_max;
@@ -807,7 +818,7 @@ struct BvhWalker {
             }
             if constexpr (kSusp) {
                 const uint64_t walking = __ballot(cur != kEnd);
-                if (walking != 0 && 64 - __popcll(walking) >= kRefetchK) break;
+                if (refetch && walking != 0 && 64 - __popcll(walking) >= kRefetchK) break;
             }
         }
         if constexpr (kSusp) {
@@ -826,7 +837,7 @@ struct BvhWalker {
 
     template <bool kSusp, class PR>
     __device__ __forceinline__ int run_f64(const Ray& r, double t_min, double t_max, double* t_hit, PR& pr, State& st,
-                                           const bool resume) const {
+                                           const bool resume, const bool refetch) const {
         const double a = len_sq(r.dir);
         double closest = t_max;
         uint32_t best = 0;
@@ -1000,7 +1011,7 @@ struct BvhWalker {
             if constexpr (kSusp) {
                 // wave-uniform: enough free lanes to make a shading batch worthwhile
                 const uint64_t walking = __ballot(cur != kEnd);
-                if (walking != 0 && 64 - __popcll(walking) >= kRefetchK) break;
+                if (refetch && walking != 0 && 64 - __popcll(walking) >= kRefetchK) break;
             }
         }
         if constexpr (kSusp) {
@@ -1234,11 +1245,11 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
         V col = V{0, 0, 0};
         Real ux = 0, uy = 0, uz = 0, uls = 1;
         bool got = false, dgot = false;
-#pragma unroll
-        for (int trip = 0; trip < kRuvTrips; ++trip) {
+        // one trip for the lanes still drawing; false when no lane of the wave is (wave-uniform)
+        auto trip = [&]() -> bool {
             const bool wr = pending && !got, wd = dpend && !dgot;
             const uint64_t need = __ballot(wr || wd);
-            if (need == 0) break;
+            if (need == 0) return false;
             if constexpr (kProf) ++n_trip;
             if constexpr (kF32) {
                 if (wr || wd) trip_f32(g, wr, ux, uy, uz, uls, got, dgot);
@@ -1254,6 +1265,17 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
                     dgot = xy + 0.0 * 0.0 < 1;  // Vec.lenSquared of (x, y, 0)
                 }
             }
+            return true;
+        };
+#pragma unroll
+        for (int k = 0; k < kRuvTrips; ++k)
+            if (!trip()) break;
+        if constexpr (kDrainMode) {
+            // drained: no lane will take a new item, so a lane left pending would only cost the wave
+            // another pass of the whole loop — draw until every lane has its sample
+            if (us.drained)
+                while (trip()) {
+                }
         }
         RTK_MARK("scatter_finish");
         if (dgot) {
@@ -1312,7 +1334,8 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
                 __builtin_amdgcn_s_setprio(2);
                 int k;
                 if constexpr (kSusp) {
-                    k = walk.template run<true>(r, (Real)p.t_min, (Real)p.t_max, &t, pr, ws, susp);
+                    k = walk.template run<true>(r, (Real)p.t_min, (Real)p.t_max, &t, pr, ws, susp,
+                                                !(kDrainMode && us.drained));
                     susp = k == kSuspended;
                 } else {
                     k = walk(r, (Real)p.t_min, (Real)p.t_max, &t, pr);

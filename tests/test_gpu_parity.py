@@ -609,3 +609,27 @@ def test_trained_tree_retrains_per_camera_across_streams(oracle, monkeypatch):
         assert np.array_equal(o2.cpu().numpy(), ref2)
     r.sync()
     r.close()
+
+
+@pytest.mark.parametrize("profile", [False, True])
+def test_direct_rows_instrumented_bit_exact(oracle, profile, monkeypatch):
+    """The launch shape of round 3's unexplained fault (profiles/r04_diag): direct-mode BVH rows of
+    an 8-rank job, plain and with the instrumented kernel writing its 32-word stats.  Bit-exact
+    against oracle B; exact sample and ray counts (reference: the row loop camera.zig:128-138 that a
+    rank's launch replaces)."""
+    import torch
+    monkeypatch.setenv("RTZIG_UNIT_MODE", "direct")
+    cam = rtzig.final_scene_camera(width=1200, aspect_ratio=1.5, spp=24)
+    r = rtzig.DeviceRenderer(0)
+    r.set_scene(cam.scene.world)
+    r.enable_profile(profile)
+    out = torch.zeros((12, 1200, 3), dtype=torch.float64, device="cuda:0")
+    stats = torch.zeros(32, dtype=torch.int64, device="cuda:0")
+    r.render_rows_async(cam.cam, out.data_ptr(), row0=3, row_step=8, n_rows=12, d_stats_ptr=stats.data_ptr())
+    r.sync()
+    assert "direct" in r.kernel_name() and ("prof" in r.kernel_name()) == profile
+    r.close()
+    ref, rays = oracle.render_b(cam.cam, cam.scene.world, row0=3, row_step=8, n_rows=12, threads=16)
+    st = stats.cpu().tolist()
+    assert np.array_equal(out.cpu().numpy(), ref)
+    assert st[0] == rays and st[1] == 12 * 1200 * 24
