@@ -386,6 +386,10 @@ constexpr int kRefetchK = RTZIG_REFETCH_K;
 #define RTZIG_DRAIN 1
 #endif
 constexpr bool kDrainMode = RTZIG_DRAIN != 0;
+#ifndef RTZIG_REFILL_MIN
+#define RTZIG_REFILL_MIN 0
+#endif
+constexpr int kRefillMin = RTZIG_REFILL_MIN;
 constexpr int kSuspended = -2;
 typedef float f2 __attribute__((ext_vector_type(2)));
 // {b.x * m.x + a.x, b.y * m.x + a.x}: v_pk_fma_f32 with the second and third operands' low halves
@@ -1049,10 +1053,12 @@ __device__ __forceinline__ void trip_f32(Rng& g, bool wr, float& ux, float& uy, 
     if (wr) {
         uz = fm::pm1(fm::uniform(g));
         uls = xy + uz * uz;
-        got = 1e-30f < uls && uls <= 1.0f;
-    } else {
-        dgot = xy < 1.0f;
     }
+    // the flags are assigned by value on both sides: stores into got OR dgot through a selected
+    // address kept both in scratch memory (8 bytes per lane, scratch_store_byte per trip)
+    const bool acc = wr ? (1e-30f < uls && uls <= 1.0f) : xy < 1.0f;
+    got = wr ? acc : got;
+    dgot = wr ? dgot : acc;
 }
 // the accepted randomUnitVec finishes a Lambertian / Metal scatter (material.zig:27-68)
 __device__ __forceinline__ void scatter_f32(float ux, float uy, float uz, float uls, bool sc_metal, fm::f3 sc_nrm,
@@ -1193,7 +1199,10 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
         bool fresh = false;
         uint32_t fq = 0, fs = 0;  // pixel (launch-local) and sample of a freshly handed item
         const bool was_drained = us.drained;
-        us.refill(active, fresh, myslot, mi, fq, fs, lane);
+        // RTZIG_REFILL_MIN (A/B knob, default 0): hand out items only once at least that many lanes
+        // are free (or the wave has no path left), so seeding / getRay run with fuller waves
+        if (kRefillMin == 0 || __popcll(__ballot(!active)) >= kRefillMin || __ballot(active) == 0)
+            us.refill(active, fresh, myslot, mi, fq, fs, lane);
         uint64_t t_ref = 0;
         if constexpr (kProf) {
             if (us.drained && !was_drained) rt_drain = __builtin_amdgcn_s_memrealtime();
@@ -1245,38 +1254,41 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
         V col = V{0, 0, 0};
         Real ux = 0, uy = 0, uz = 0, uls = 1;
         bool got = false, dgot = false;
-        // one trip for the lanes still drawing; false when no lane of the wave is (wave-uniform)
-        auto trip = [&]() -> bool {
-            const bool wr = pending && !got, wd = dpend && !dgot;
-            const uint64_t need = __ballot(wr || wd);
-            if (need == 0) return false;
-            if constexpr (kProf) ++n_trip;
-            if constexpr (kF32) {
-                if (wr || wd) trip_f32(g, wr, ux, uy, uz, uls, got, dgot);
-            } else if (wr || wd) {
-                ux = g.range_pm1();
-                uy = g.range_pm1();
-                const double xy = ux * ux + uy * uy;
-                if (wr) {
-                    uz = g.range_pm1();
-                    uls = xy + uz * uz;
-                    got = 1e-160 < uls && uls <= 1;
-                } else {
-                    dgot = xy + 0.0 * 0.0 < 1;  // Vec.lenSquared of (x, y, 0)
-                }
-            }
-            return true;
-        };
+        // One trip for the lanes still drawing; leaves the loop when no lane of the wave is.  (A macro:
+        // written as a lambda or a function taking the flags by reference, got / dgot went to
+        // scratch memory.)
+#define RTK_TRIP_BODY                                                                   \
+    const bool wr = pending && !got, wd = dpend && !dgot;                               \
+    if (__ballot(wr || wd) == 0) break;                                                 \
+    if constexpr (kProf) ++n_trip;                                                      \
+    if constexpr (kF32) {                                                               \
+        if (wr || wd) trip_f32(g, wr, ux, uy, uz, uls, got, dgot);                      \
+    } else if (wr || wd) {                                                              \
+        ux = g.range_pm1();                                                             \
+        uy = g.range_pm1();                                                             \
+        const double xy = ux * ux + uy * uy;                                            \
+        if (wr) {                                                                       \
+            uz = g.range_pm1();                                                         \
+            uls = xy + uz * uz;                                                         \
+        }                                                                               \
+        /* Vec.lenSquared of (x, y, 0) for the disk; flags assigned by value (see trip_f32) */ \
+        const bool acc = wr ? (1e-160 < uls && uls <= 1) : xy + 0.0 * 0.0 < 1;         \
+        got = wr ? acc : got;                                                           \
+        dgot = wr ? dgot : acc;                                                         \
+    }
 #pragma unroll
-        for (int k = 0; k < kRuvTrips; ++k)
-            if (!trip()) break;
+        for (int k = 0; k < kRuvTrips; ++k) {
+            RTK_TRIP_BODY
+        }
         if constexpr (kDrainMode) {
             // drained: no lane will take a new item, so a lane left pending would only cost the wave
             // another pass of the whole loop — draw until every lane has its sample
             if (us.drained)
-                while (trip()) {
+                while (true) {
+                    RTK_TRIP_BODY
                 }
         }
+#undef RTK_TRIP_BODY
         RTK_MARK("scatter_finish");
         if (dgot) {
             camera_finish(ux, uy, r);

@@ -128,7 +128,7 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(kWaves, kWave
 // lane whose path has ended takes the wave's next path (ballot + mbcnt, no atomics).  Dynamic fetch as
 // in the product.  The static-stride kernel above gives neighbouring lanes consecutive segments of ONE
 // path (a camera ray next to its own bounces), which the megakernel never does.
-template <int B, class StackT, int kWaves>
+template <int B, class StackT, int kWaves, bool kPrefetch = false>
 __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(kWaves, kWaves))) void walk_kernel_paths(
     KernelParams kp_unused, BvhArgs b, Segs sg, double t_min, int32_t* __restrict__ out_k,
     double* __restrict__ out_t, unsigned long long* __restrict__ ctr, unsigned long long* __restrict__ sum) {
@@ -151,7 +151,8 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(kWaves, kWave
     const uint32_t pend = pnext + per < sg.total_paths ? pnext + per : sg.total_paths;
     bool active = false, susp = false, has_path = false;
     uint32_t seg = 0, seg_end = 0, rep = 0;  // the lane's current segment, its path's end, replay round
-    Ray r;
+    Ray r, nr;                               // nr: the next segment, prefetched (kPrefetch)
+    bool pf_ok = false;                      // nr holds segment seg's ray
     typename W::State ws;
     Prof<false> pr;
     uint64_t check = 0;
@@ -171,8 +172,23 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(kWaves, kWave
             pnext = pnext + got < pend ? pnext + got : pend;
         }
         if (has_path && !active) {
-            r.orig = mk(sg.ox[seg], sg.oy[seg], sg.oz[seg]);
-            r.dir = mk(sg.dx[seg], sg.dy[seg], sg.dz[seg]);
+            if constexpr (kPrefetch) {
+                // the ray was loaded into nr while the previous segment walked (the megakernel has
+                // it in registers from shading); a new path's first segment is loaded here
+                if (!pf_ok) {
+                    nr.orig = mk(sg.ox[seg], sg.oy[seg], sg.oz[seg]);
+                    nr.dir = mk(sg.dx[seg], sg.dy[seg], sg.dz[seg]);
+                }
+                r = nr;
+                if (seg + 1 < seg_end) {
+                    nr.orig = mk(sg.ox[seg + 1], sg.oy[seg + 1], sg.oz[seg + 1]);
+                    nr.dir = mk(sg.dx[seg + 1], sg.dy[seg + 1], sg.dz[seg + 1]);
+                }
+                pf_ok = seg + 1 < seg_end;
+            } else {
+                r.orig = mk(sg.ox[seg], sg.oy[seg], sg.oz[seg]);
+                r.dir = mk(sg.dx[seg], sg.dy[seg], sg.dz[seg]);
+            }
             active = true;
             susp = false;
         }
@@ -191,7 +207,10 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(kWaves, kWave
                     check += (uint64_t)(k + 1) + __builtin_bit_cast(uint64_t, t);
                 }
                 active = false;
-                if (++seg == seg_end) has_path = false;
+                if (++seg == seg_end) {
+                    has_path = false;
+                    pf_ok = false;
+                }
             }
         }
     }
@@ -429,6 +448,9 @@ int main(int argc, char** argv) {
         run(occ::walk_kernel_paths<512, int16_t, 4>, "paths_w4_i16", 512, 4, 2);
         run(occ::walk_kernel_paths<640, int16_t, 5>, "paths_w5_i16", 640, 5, 2);
         run(occ::walk_kernel_paths<768, int16_t, 6>, "paths_w6_i16", 768, 6, 2);
+        run(occ::walk_kernel_paths<512, int32_t, 4, true>, "paths_pf_w4_i32", 512, 4, 4);
+        run(occ::walk_kernel_paths<640, int16_t, 5, true>, "paths_pf_w5_i16", 640, 5, 2);
+        // (6 waves with prefetch needs 94 VGPRs of 80 and spills 14 to scratch: not run, as w8 above)
     }
 
     // host check of a sample against the reference's linear scan
