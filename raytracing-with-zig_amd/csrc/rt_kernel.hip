@@ -383,9 +383,10 @@ constexpr int kRefetchK = RTZIG_REFETCH_K;
 // every lane has its sample instead of kRuvTrips trips per iteration, so the paths still in flight
 // at the end of a launch take fewer loop iterations (the drain tail).  Results unchanged.
 #ifndef RTZIG_DRAIN
-#define RTZIG_DRAIN 1
+#define RTZIG_DRAIN 0
 #endif
-constexpr bool kDrainMode = RTZIG_DRAIN != 0;
+constexpr bool kDrainMode = RTZIG_DRAIN != 0;     // drained walks do not suspend
+constexpr bool kDrainTrips = RTZIG_DRAIN == 1;    // drained trips are not capped (RTZIG_DRAIN=2: walks only)
 #ifndef RTZIG_REFILL_MIN
 #define RTZIG_REFILL_MIN 0
 #endif
@@ -1280,7 +1281,7 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
         for (int k = 0; k < kRuvTrips; ++k) {
             RTK_TRIP_BODY
         }
-        if constexpr (kDrainMode) {
+        if constexpr (kDrainTrips) {
             // drained: no lane will take a new item, so a lane left pending would only cost the wave
             // another pass of the whole loop — draw until every lane has its sample
             if (us.drained)
