@@ -336,7 +336,23 @@ struct LinearWalker {
 // v_max/v_min.  With IEEE mode on (the default) these return the non-NaN operand for quiet NaNs —
 // exactly fmaxf/fminf on every value this walk produces (arithmetic never yields signaling NaNs) —
 // but written as builtins the compiler re-canonicalizes the loop-carried bounds every iteration.
-#if RTZIG_WALK_FORM >= 1
+#ifndef RTZIG_WALK_FORM
+#define RTZIG_WALK_FORM 0
+#endif
+#if RTZIG_WALK_FORM == 4
+__device__ __forceinline__ float slab_near(float x, float y, float z, float lower) {
+    float t, r;
+    asm("v_max_f32 %0, %1, %2" : "=v"(t) : "v"(z), "v"(lower));
+    asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(x), "v"(y), "v"(t));
+    return r;
+}
+__device__ __forceinline__ float slab_far(float x, float y, float z, float upper) {
+    float t, r;
+    asm("v_min_f32 %0, %1, %2" : "=v"(t) : "v"(z), "v"(upper));
+    asm("v_min3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(x), "v"(y), "v"(t));
+    return r;
+}
+#elif RTZIG_WALK_FORM >= 1
 __device__ __forceinline__ float slab_near(float x, float y, float z, float lower) {
     return __builtin_fmaxf(__builtin_fmaxf(x, y), __builtin_fmaxf(z, lower));
 }
@@ -395,11 +411,17 @@ constexpr int kSuspended = -2;
 typedef float f2 __attribute__((ext_vector_type(2)));
 // {b.x * m.x + a.x, b.y * m.x + a.x}: v_pk_fma_f32 with the second and third operands' low halves
 // broadcast to the high lane (op_sel_hi:[1,0,0]); their high halves are never read
-#ifndef RTZIG_WALK_FORM
-#define RTZIG_WALK_FORM 0
+// Forms of the inner step (A/B knob): 0 the shipped one (inline-asm v_pk_fma_f32 with a
+// broadcast operand, volatile-asm v_max3/v_min3, asm ds_read_b64); 1 builtin packed fma and
+// min/max; 2 form 1 with plain LDS loads (ds_read2_b64); 4 form 0 with the slab min/max as
+// non-volatile asm (schedulable); 5 form 0 with builtin min/max.
+#if RTZIG_WALK_FORM == 4 || RTZIG_WALK_FORM == 5
+#define RTK_PK_ASM 1
+#else
+#define RTK_PK_ASM (RTZIG_WALK_FORM == 0)
 #endif
 __device__ __forceinline__ f2 pk_fma_lo(f2 b, f2 m, f2 a) {
-#if RTZIG_WALK_FORM >= 1
+#if !RTK_PK_ASM
     const f2 mm = {m.x, m.x}, aa = {a.x, a.x};
     return __builtin_elementwise_fma(b, mm, aa);
 #else
@@ -690,7 +712,7 @@ struct BvhWalker {
             pr.inner_iter();
             f2 bx0, by0, bz0, bx1, by1, bz1;
             int32_t ref0, ref1, popped;
-            if constexpr (kLdsNodes && RTZIG_WALK_FORM < 2) {
+            if constexpr (kLdsNodes && RTZIG_WALK_FORM != 2 && RTZIG_WALK_FORM != 3) {
                 // nodes start at LDS address 0: the ref is the address.  Seven ds_read_b64
                 // (2 LDS cycles each); left to itself the compiler pairs them into
                 // ds_read2_b64 (8 cycles for the same 16 B) behind extra base adds.
@@ -743,7 +765,7 @@ struct BvhWalker {
             // The three compares are taken as wave masks and combined on the scalar unit, and
             // the selects are v_cndmask on those masks: 3 compares + 5 selects (the compiler's
             // form of the same logic re-compared a negated mask on the VALU).
-#if RTZIG_WALK_FORM >= 3
+#if RTZIG_WALK_FORM == 3
             const bool h0 = n0 <= f0, h1 = n1 <= f1, nf = n0 <= n1;
             const bool p0 = h0 && (!h1 || nf);
             const int32_t near = p0 ? ref0 : ref1, far = p0 ? ref1 : ref0;

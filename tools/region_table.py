@@ -11,7 +11,8 @@
 3. Counts each region's instructions by class (f64 VALU, 32-bit VALU, SALU, LDS, VMEM, s_nop) on its
    common path (rare blocks apart) and weights them with the wave-level executions of one
    instrumented frame (tools/kprofile.py --spp 100 -> stats[7..10], [26..31]):
-     finalise, handout, idle, store: once per loop iteration; seed: seeding blocks; trips: trips;
+     finalise, handout, idle, store: once per loop iteration; seed: seeding blocks; trips: the three
+     unrolled trips' blocks, each once per trip (region static count x trips / 3);
      scatter_finish: per iteration; walk_setup: walks started; walk_inner: the inner-step loop block
      per inner step, its other blocks per leaf round + walk start; leaf: per leaf round, with the
      sqrt/root blocks per candidate block; shade: shading blocks; fin_work (the ring fold of a unit
@@ -151,6 +152,18 @@ def main():
     inner_loop = {k for k, ss in succ.items() if k in ss and any(klass(i) == "lds" for i in blocks[k]["ins"])
                   and any(i.startswith("v_pk_fma") for i in blocks[k]["ins"])}
     cand_blocks = {k for k, b in enumerate(blocks) if any(i.startswith("v_rsq_f64") for i in b["ins"])}
+    # blocks on a cycle that stays inside walk_setup: the always-list loop for more than 4 spheres
+    ws_blocks = {k for k, r, _ in per if r == "walk_setup"}
+    def reach(a):
+        seen, todo = set(), [a]
+        while todo:
+            x = todo.pop()
+            for y in succ.get(x, []):
+                if y in ws_blocks and y not in seen:
+                    seen.add(y)
+                    todo.append(y)
+        return seen
+    ws_loop = {k for k in ws_blocks if k in reach(k)}
     dyn = collections.defaultdict(lambda: collections.Counter())
     for k, r, ins in per:
         c = klass(ins)
@@ -162,9 +175,12 @@ def main():
         elif r == "leaf":
             w = n["cand"] - 0.0 if k in cand_blocks else n["leaf"]
         elif r == "walk_setup":
-            w = n["wstart"]
+            # the always-list loop for more than 4 spheres (self-loop blocks) does not run on a scene
+            # with <= 4 always-list spheres (config 4: the ground and three r = 1 spheres)
+            w = 0 if k in ws_loop else n["wstart"]
         elif r == "trips":
-            w = n["trips"]
+            # the region holds kRuvTrips = 3 unrolled trips: each trip's blocks run once per trip
+            w = n["trips"] / 3
         elif r == "seed":
             w = n["seed"]
         elif r == "shade":
