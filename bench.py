@@ -396,8 +396,10 @@ def run(args):
             cyc = pmc["valu_issue_cycles_per_frame"]
             issue = {"frac": round(cyc / (SIMDS * pmc["clock_GHz"] * 1e9 * k_frame_s), 4),
                      "valu_issue_cycles_per_frame": cyc, "clock_GHz": pmc["clock_GHz"],
-                     "model": "2 cycles per wave64 32-bit VALU op, 4 per f64 add/mul/fma, 8 per "
-                              "transcendental (MI355X_MICROARCH.md), / (1024 SIMDs x clock x kernel time)",
+                     "model": "PMC VALU counts x issue cycles per wave64 instruction MEASURED on the MI355X at "
+                              "4 waves/SIMD (f64 add/mul/fma 2.12, rsq/rcp_f64 7.94, rcp_f32 6.03, the other "
+                              "ops at the kernel's own measured-rate mix), / (1024 SIMDs x clock x kernel time)",
+                     "rates": pmc.get("valu_issue_model"),
                      "source": pmc.get("source")}
         # HBM: the algorithmic traffic of a frame is the f64 linear framebuffer W*H*24 (or W*H*3
         # bytes of RGB8) written once; the rest is the design's own: each sample's

@@ -11,9 +11,18 @@ launches (sample chunks); every counter is summed over the timed kernel's dispat
 Units (MI355X_MICROARCH.md): FETCH_SIZE / WRITE_SIZE in KiB; SQ_WAVE_CYCLES, SQ_WAIT_*,
 SQ_ACTIVE_INST_* and SQ_BUSY_CYCLES count quad-cycles; SQ_INSTS_* count wave-instructions; the
 effective clock is GRBM_GUI_ACTIVE / 8 XCDs / the kernel's wall time.
-VALU issue model (the guide: a wave64 VALU instruction issues over 2 cycles on a SIMD-32; f64
-add/mul/fma at half rate, 4 cycles; transcendentals 8):
-    issue cycles = 2 * n_32bit + 4 * n_f64 + 8 * n_trans,   frac = issue / (1024 SIMDs x clock x t)
+VALU issue model, MEASURED on the MI355X (round 4, tools/valu_rates.hip,
+profiles/r04_valu_rates/): SIMD cycles per wave64 instruction at the kernel's 4 waves per SIMD.
+f64 add/mul/fma issue at 2.12 (full rate on CDNA4, not half), rsq/rcp_f64 at 7.94, rcp_f32 at 6.03;
+the other 32/64-bit ops split into a 2.0 class (add, xor, and, mov, bitop3, 64-bit shifts, f64
+compares) and a 3.0-3.1 class (32-bit min/max/compare/cndmask, alignbit, mul_lo, mad_u64_u32, bfi).
+The mix of the latter comes from the kernel's own instruction stream: profiles/<tag>/region_table.json
+(tools/region_table.py) prices every opcode of the shipped kernel with its measured rate, weighted by
+the exact per-region executions of one instrumented frame; its mean cycles per VALU instruction of the
+non-f64, non-transcendental ops prices the PMC's "other" count:
+    issue cycles = 2.12 n_f64 + 7.94 n_trans_f64 + 6.03 n_trans_f32 + r_other n_other,
+    frac = issue / (1024 SIMDs x clock x t)
+(rounds 1-3 used the guide's nominal 2 / 4 / 8 cycles, which overprices f64 by 2x.)
 """
 import csv
 import glob
@@ -84,12 +93,21 @@ def main(tag, workload):
         out["clock_GHz"] = clock / 1e9
         if "SQ_INSTS_VALU_ADD_F64" in sums and "SQ_INSTS_VALU" in sums:
             n64 = g("SQ_INSTS_VALU_ADD_F64") + g("SQ_INSTS_VALU_MUL_F64") + g("SQ_INSTS_VALU_FMA_F64")
-            ntr = g("SQ_INSTS_VALU_TRANS_F32") + g("SQ_INSTS_VALU_TRANS_F64")
-            n32 = g("SQ_INSTS_VALU") - n64 - ntr
-            cyc = 2 * n32 + 4 * n64 + 8 * ntr
+            ntr64, ntr32 = g("SQ_INSTS_VALU_TRANS_F64"), g("SQ_INSTS_VALU_TRANS_F32")
+            n32 = g("SQ_INSTS_VALU") - n64 - ntr64 - ntr32
+            r_other, src_other = 2.6, "assumed (no region table for this tag)"
+            rtab = os.path.join(dst, "region_table.json")
+            if os.path.exists(rtab):
+                r_other = json.load(open(rtab))["total_est"]["other_valu_cycles_per_instruction"]
+                src_other = f"profiles/{tag}/region_table.json"
+            cyc = 2.12 * n64 + 7.94 * ntr64 + 6.03 * ntr32 + r_other * n32
             out["valu_issue_cycles_per_frame"] = cyc
             out["valu_issue_frac_pmc_pass"] = cyc / (SIMDS * clock * T)
-            out["valu_insts"] = {"total": g("SQ_INSTS_VALU"), "f64": n64, "trans": ntr, "other_32bit": n32}
+            out["valu_issue_model"] = {"f64_add_mul_fma": 2.12, "trans_f64": 7.94, "trans_f32": 6.03,
+                                       "other": round(r_other, 4), "other_source": src_other,
+                                       "rates": "profiles/r04_valu_rates/valu_rates_b.json"}
+            out["valu_issue_cycles_nominal_guide_model"] = 2 * n32 + 4 * n64 + 8 * (ntr64 + ntr32)
+            out["valu_insts"] = {"total": g("SQ_INSTS_VALU"), "f64": n64, "trans": ntr64 + ntr32, "other_32bit": n32}
         if "SQ_WAVE_CYCLES" in sums and "SQ_ACTIVE_INST_ANY" in sums:
             wc = g("SQ_WAVE_CYCLES")
             out["wave_cycle_split"] = {"active_inst_any": g("SQ_ACTIVE_INST_ANY") / wc,
@@ -110,7 +128,7 @@ def main(tag, workload):
     json.dump(out, open(os.path.join(dst, "summary.json"), "w"), indent=1)
     if "hbm_bytes_per_frame" in out:
         keep = {k: out[k] for k in ("workload", "tag", "launches_per_frame", "hbm_bytes_per_frame", "fetch_bytes_per_frame",
-                                    "write_bytes_per_frame", "valu_issue_cycles_per_frame", "clock_GHz") if k in out}
+                                    "write_bytes_per_frame", "valu_issue_cycles_per_frame", "valu_issue_model", "clock_GHz") if k in out}
         keep["source"] = (f"profiles/{tag}/summary.json (rocprofv3 --pmc, separate passes; FETCH_SIZE + WRITE_SIZE "
                           "KiB x 1024, summed over the frame's sample-kernel launches)")
         json.dump(keep, open(os.path.join(ROOT, "profiles", "pmc_traffic.json"), "w"), indent=1)

@@ -20,8 +20,13 @@
    Every block of a region is assumed to run whenever the region runs (a wave executes each branch
    some lane takes), so the estimate is an upper bound per region; the sum is compared with the
    PMC count of VALU instructions.
+4. Prices every VALU opcode with its MEASURED issue cost on the MI355X (tools/valu_rates.hip,
+   profiles/r04_valu_rates/valu_rates_b.json: SIMD cycles per wave64 instruction with 4 waves per
+   SIMD, the kernel's occupancy): e.g. f64 add/mul/fma/max/compare, 32-bit add/xor/and/mov, bitop3,
+   pk_fma 1.9-2.1; 32-bit min/max/compare/cndmask, alignbit, mul_lo, mad_u64_u32, bfi, lshlrev_b32
+   3.0-3.1; rcp_f32 6.0; rsq/rcp_f64 7.9.  An opcode the table lacks takes its class's rate.
 
-    python tools/region_table.py <kprof.json> [--spp-scale 5] [--pmc profiles/r03/summary.json] [--out F]
+    python tools/region_table.py <kprof.json> [--spp-scale 5] [--pmc profiles/r04/summary.json] [--out F]
 """
 import argparse
 import collections
@@ -35,6 +40,40 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SRC = os.path.join(ROOT, "raytracing-with-zig_amd", "csrc", "rt_kernel.hip")
 KERNEL = "_ZN3rtk17sample_kernel_bvhILb1ELb0ELb0E"
 F64 = re.compile(r"^v_(add|mul|fma|fmac)_f64|^v_(rsq|rcp|sqrt)_f64|^v_div_(scale|fmas|fixup)_f64|^v_cmp\w*_f64|^v_(min|max)_f64|^v_cvt_f64")
+
+
+RATES = os.path.join(ROOT, "profiles", "r04_valu_rates", "valu_rates_b.json")
+
+
+def load_rates(path=RATES):
+    """opcode -> SIMD cycles per wave64 instruction at 4 waves/SIMD (measured)."""
+    out = {}
+    for r in json.load(open(path))["results"]:
+        op = r["op"].split()[0]
+        if op == "v_cndmask_b32":  # VOP2 form reading a VCC nothing wrote: an artifact (README); use the e64 rate
+            continue
+        out[op] = r["simd_cycles_per_instr_4waves"]
+    out["v_cndmask_b32"] = out.get("v_cndmask_b32_e64", 3.12)
+    return out
+
+
+def rate(op, rates):
+    """Issue cost of one opcode: exact match (encoding suffix dropped), else a measured sibling."""
+    base = re.sub(r"_(e32|e64|sdwa|dpp)$", "", op)
+    if base in rates:
+        return rates[base]
+    sib = [("v_fmac_f64", "v_fma_f64"), ("v_fmac_f32", "v_fma_f32"), ("v_cmp", "v_cmp_lt_f64" if "f64" in base or "64" in base else "v_cmp_gt_f32"),
+           ("v_cndmask", "v_cndmask_b32_e64"), ("v_min3", "v_max3_f32"), ("v_max3", "v_max3_f32"), ("v_min_f64", "v_max_f64"),
+           ("v_or_b32", "v_xor_b32"), ("v_sub_", "v_sub_u32"), ("v_subrev", "v_sub_u32"), ("v_addc", "v_add_co_u32"),
+           ("v_sub_co", "v_add_co_u32"), ("v_readlane", "v_mbcnt_lo_u32_b32"), ("v_readfirstlane", "v_mbcnt_lo_u32_b32"),
+           ("v_writelane", "v_mbcnt_lo_u32_b32"), ("v_mbcnt", "v_mbcnt_lo_u32_b32"), ("v_cvt", "v_cvt_f32_f64"),
+           ("v_rsq", "v_rsq_f64"), ("v_sqrt_f64", "v_rsq_f64"), ("v_div_", "v_fma_f64"), ("v_frexp", "v_ldexp_f64"),
+           ("v_mul_f64", "v_mul_f64"), ("v_pk_", "v_pk_fma_f32"), ("v_mov", "v_mov_b32"), ("v_lshl_or", "v_and_or_b32"),
+           ("v_or3", "v_and_or_b32"), ("v_ashrrev_i64", "v_lshrrev_b64"), ("v_min_u32", "v_max_u32"), ("v_min_i32", "v_max_i32")]
+    for pre, tgt in sib:
+        if base.startswith(pre) and tgt in rates:
+            return rates[tgt]
+    return 3.12 if base.startswith("v_") else 0.0
 
 
 def asm(extra):
@@ -138,7 +177,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("kprof")
     ap.add_argument("--spp-scale", type=float, default=5.0, help="frame spp / kprof spp (500 / 100)")
-    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r03", "summary.json"))
+    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r04", "summary.json"))
     ap.add_argument("--out", default=None)
     ap.add_argument("-D", action="append", default=[], help="extra -D for the build (variants)")
     args = ap.parse_args()
@@ -165,6 +204,11 @@ def main():
         return seen
     ws_loop = {k for k in ws_blocks if k in reach(k)}
     dyn = collections.defaultdict(lambda: collections.Counter())
+    rates = load_rates()
+    cyc = collections.Counter()    # measured-rate VALU issue cycles per region
+    other = collections.Counter()  # the ops outside the PMC's f64 add/mul/fma and transcendental classes
+    opcyc = collections.Counter()  # ... per opcode (whole kernel)
+    unpriced = collections.Counter()
     for k, r, ins in per:
         c = klass(ins)
         static[r][c] += 1
@@ -191,6 +235,18 @@ def main():
         else:
             w = n["iter"]
         dyn[r][c] += w
+        op = ins.split()[0]
+        if op.startswith("v_"):
+            rt = rate(op, rates)
+            base = re.sub(r"_(e32|e64|sdwa|dpp)$", "", op)
+            if base not in rates:
+                unpriced[op] += w
+            cyc[r] += w * rt
+            opcyc[op] += w * rt
+            if r not in ("rare", "prologue", "epilogue", "?") and not re.match(
+                    r"^v_(add|mul|fma|fmac)_f64|^v_(rsq|rcp|sqrt|exp|log|sin|cos)_f(32|64)", op):
+                other["n"] += w
+                other["cyc"] += w * rt
     order = ["finalise", "fin_work", "handout", "seed", "idle", "trips", "scatter_finish", "walk_setup", "walk_inner", "leaf", "shade",
              "store", "rare", "prologue", "epilogue", "?"]
     rows = []
@@ -200,30 +256,41 @@ def main():
             continue
         d = dyn.get(r, collections.Counter())
         tot.update(d)
-        issue = 2 * d["valu_32"] + 4 * d["valu_f64"]
         rows.append({"region": r, "static": dict(static[r]),
-                     "executions_per_frame": None if r in ("rare", "prologue", "?") else None,
                      "dyn_valu": d["valu_32"] + d["valu_f64"], "dyn_valu_f64": d["valu_f64"], "dyn_salu": d["salu"],
-                     "dyn_lds": d["lds"], "dyn_nop": d["nop"], "valu_issue_cycles_est": issue})
+                     "dyn_lds": d["lds"], "dyn_nop": d["nop"], "valu_issue_cycles_est": cyc.get(r, 0.0)})
+    tcyc = sum(cyc[r["region"]] for r in rows)
+    tval = tot["valu_32"] + tot["valu_f64"]
+    for r in rows:
+        r["valu_issue_share"] = round(r["valu_issue_cycles_est"] / tcyc, 4) if tcyc else None
     res = {"kernel": "sample_kernel_bvh<true,false,false> (-DRTZIG_MARKS=1 build: " + str(len(per)) + " instructions)",
            "counts_per_frame": n, "rows": rows,
-           "total_est": {"valu": tot["valu_32"] + tot["valu_f64"], "valu_f64": tot["valu_f64"], "salu": tot["salu"],
-                         "lds": tot["lds"], "nop": tot["nop"]}}
+           "total_est": {"valu": tval, "valu_f64": tot["valu_f64"], "salu": tot["salu"],
+                         "lds": tot["lds"], "nop": tot["nop"], "valu_issue_cycles": tcyc,
+                         "valu_cycles_per_instruction": tcyc / tval if tval else None,
+                         "other_valu_cycles_per_instruction": other["cyc"] / other["n"] if other["n"] else None},
+           "rates": {"source": os.path.relpath(RATES, ROOT),
+                     "model": "SIMD cycles per wave64 instruction at 4 waves/SIMD, measured per opcode"},
+           "top_opcodes_by_issue_cycles": [{"op": o, "cycles": c, "share": round(c / tcyc, 4), "rate": rate(o, rates)}
+                                           for o, c in opcyc.most_common(25)],
+           "unpriced_opcodes (sibling rate used)": {o: c for o, c in unpriced.most_common(10)}}
     try:
         pm = json.load(open(args.pmc))["counters_per_frame"]
         res["pmc"] = {"valu": pm["SQ_INSTS_VALU"], "salu": pm["SQ_INSTS_SALU"], "lds": pm["SQ_INSTS_LDS"],
                       "valu_f64": pm["SQ_INSTS_VALU_ADD_F64"] + pm["SQ_INSTS_VALU_MUL_F64"] + pm["SQ_INSTS_VALU_FMA_F64"],
-                      "source": args.pmc}
+                      "source": os.path.relpath(args.pmc, ROOT),
+                      "estimate_over_pmc_valu": round(tval / pm["SQ_INSTS_VALU"], 3)}
     except (OSError, KeyError):
         pass
     txt = json.dumps(res, indent=1)
     if args.out:
         open(args.out, "w").write(txt)
-    print(f"{'region':16s} {'static V/S/LDS/nop':>22s} {'dyn VALU':>10s} {'f64':>9s} {'SALU':>9s} {'LDS':>9s} {'issue cyc':>10s}")
+    print(f"{'region':16s} {'static V/S/LDS/nop':>22s} {'dyn VALU':>10s} {'f64':>9s} {'SALU':>9s} {'LDS':>9s} {'issue cyc':>10s} share")
     for r in rows:
         s = r["static"]
         print(f"{r['region']:16s} {s.get('valu_32', 0) + s.get('valu_f64', 0):5d}/{s.get('salu', 0):4d}/{s.get('lds', 0):3d}/{s.get('nop', 0):3d}"
-              f"       {r['dyn_valu']:10.3g} {r['dyn_valu_f64']:9.3g} {r['dyn_salu']:9.3g} {r['dyn_lds']:9.3g} {r['valu_issue_cycles_est']:10.3g}")
+              f"       {r['dyn_valu']:10.3g} {r['dyn_valu_f64']:9.3g} {r['dyn_salu']:9.3g} {r['dyn_lds']:9.3g} {r['valu_issue_cycles_est']:10.3g}"
+              f" {r['valu_issue_share'] or 0:.3f}")
     print("total est", res["total_est"], "pmc", res.get("pmc"))
 
 

@@ -95,6 +95,37 @@ __device__ __forceinline__ double fold(T x) { return (double)x; }
 #define I_LSHL_B32(X) "v_lshlrev_b32 " X ", 7, " X "\n"
 #define I_BFI(X) "v_bfi_b32 " X ", %8, " X ", %9\n"
 #define I_CVT_F32_F64(X) "v_cvt_f32_f64 " X ", %8\n"
+#define I_ADD3(X) "v_add3_u32 " X ", " X ", %8, %9\n"
+#define I_LSHL_ADD_U32(X) "v_lshl_add_u32 " X ", " X ", 2, %8\n"
+#define I_MBCNT(X) "v_mbcnt_lo_u32_b32 " X ", %8, " X "\n"
+#define I_RCP_F32(X) "v_rcp_f32 " X ", " X "\n"
+#define I_RCP_F64(X) "v_rcp_f64 " X ", " X "\n"
+#define I_LDEXP_F64(X) "v_ldexp_f64 " X ", " X ", 1\n"
+#define I_BFREV(X) "v_bfrev_b32 " X ", " X "\n"
+#define I_AND_OR(X) "v_and_or_b32 " X ", " X ", %8, %9\n"
+#define I_NOT(X) "v_not_b32 " X ", " X "\n"
+#define I_ADD_CO(X) "v_add_co_u32 " X ", vcc, " X ", %8\n"
+#define I_MOV_B64(X) "v_mov_b64 " X ", %8\n"
+#define I_MAX_F64(X) "v_max_f64 " X ", " X ", %8\n"
+#define I_CMP_F64(X) "v_cmp_lt_f64 vcc, " X ", %8\n"
+#define I_CMP_U64(X) "v_cmp_gt_u64 vcc, " X ", %8\n"
+#define I_LSHR_B32(X) "v_lshrrev_b32 " X ", 7, " X "\n"
+#define I_AND_B32(X) "v_and_b32 " X ", " X ", %8\n"
+#define I_LSHL_B64(X) "v_lshlrev_b64 " X ", 7, " X "\n"
+#define I_MUL_F32(X) "v_mul_f32 " X ", " X ", %8\n"
+#define I_SUB_U32(X) "v_sub_u32 " X ", " X ", %8\n"
+#define I_MAX_I32(X) "v_max_i32 " X ", " X ", %8\n"
+#define I_MIN_I32(X) "v_min_i32 " X ", " X ", %8\n"
+#define I_MAX3_I32(X) "v_max3_i32 " X ", " X ", %8, %9\n"
+#define I_MIN3_I32(X) "v_min3_i32 " X ", " X ", %8, %9\n"
+#define I_MAX_U32(X) "v_max_u32 " X ", " X ", %8\n"
+#define I_CMP_LE_I32(X) "v_cmp_le_i32 vcc, " X ", %8\n"
+#define I_CMP_LE_I32_S(X) "v_cmp_le_i32_e64 %10, " X ", %8\n"
+#define I_MAXIMUM3_F32(X) "v_maximum3_f32 " X ", " X ", %8, %9\n"
+#define I_MIN_F32(X) "v_min_f32 " X ", " X ", %8\n"
+#define I_SUB_F32(X) "v_sub_f32 " X ", " X ", %8\n"
+#define I_PK_ADD_F32(X) "v_pk_add_f32 " X ", " X ", %8\n"
+#define I_ASHR_I32(X) "v_ashrrev_i32 " X ", 31, " X "\n"
 
 KERNEL(add_f64, double, I_ADD_F64) KERNEL(mul_f64, double, I_MUL_F64) KERNEL(fma_f64, double, I_FMA_F64)
 KERNEL(rsq_f64, double, I_RSQ_F64) KERNEL(lshl_add_u64, double, I_LSHL_ADD_U64) KERNEL(lshr_b64, double, I_LSHR_B64)
@@ -105,6 +136,17 @@ KERNEL(ffbh, uint32_t, I_FFBH) KERNEL(mad_i32_i24, uint32_t, I_MAD_I32_I24)
 KERNEL(cndmask_s, uint32_t, I_CNDMASK_S) KERNEL(cndmask_vcmp, uint32_t, I_CNDMASK_VCMP) KERNEL(cmp_f32, uint32_t, I_CMP_F32)
 KERNEL(mov, uint32_t, I_MOV) KERNEL(xor32, uint32_t, I_XOR) KERNEL(max_f32, uint32_t, I_MAX_F32)
 KERNEL(med3_f32, uint32_t, I_MED3_F32) KERNEL(lshl_b32, uint32_t, I_LSHL_B32) KERNEL(bfi, uint32_t, I_BFI)
+KERNEL(add3, uint32_t, I_ADD3) KERNEL(lshl_add_u32, uint32_t, I_LSHL_ADD_U32) KERNEL(mbcnt, uint32_t, I_MBCNT)
+KERNEL(rcp_f32, uint32_t, I_RCP_F32) KERNEL(rcp_f64, double, I_RCP_F64) KERNEL(ldexp_f64, double, I_LDEXP_F64)
+KERNEL(bfrev, uint32_t, I_BFREV) KERNEL(and_or, uint32_t, I_AND_OR) KERNEL(not32, uint32_t, I_NOT)
+KERNEL(add_co, uint32_t, I_ADD_CO) KERNEL(mov_b64, double, I_MOV_B64) KERNEL(max_f64, double, I_MAX_F64)
+KERNEL(cmp_f64, double, I_CMP_F64) KERNEL(cmp_u64, double, I_CMP_U64) KERNEL(lshr_b32, uint32_t, I_LSHR_B32)
+KERNEL(and32, uint32_t, I_AND_B32) KERNEL(lshl_b64, double, I_LSHL_B64) KERNEL(mul_f32, uint32_t, I_MUL_F32)
+KERNEL(sub_u32, uint32_t, I_SUB_U32)
+KERNEL(max_i32, uint32_t, I_MAX_I32) KERNEL(min_i32, uint32_t, I_MIN_I32) KERNEL(max3_i32, uint32_t, I_MAX3_I32)
+KERNEL(min3_i32, uint32_t, I_MIN3_I32) KERNEL(max_u32, uint32_t, I_MAX_U32) KERNEL(cmp_le_i32, uint32_t, I_CMP_LE_I32)
+KERNEL(maximum3_f32, uint32_t, I_MAXIMUM3_F32) KERNEL(min_f32, uint32_t, I_MIN_F32)
+KERNEL(sub_f32, uint32_t, I_SUB_F32) KERNEL(pk_add_f32, double, I_PK_ADD_F32) KERNEL(ashr_i32, uint32_t, I_ASHR_I32)
 // v_mad_u64_u32: 32 x 32 -> 64 plus a 64-bit addend, into a pair
 __global__ void k_mad_u64_u32(unsigned long long* cyc, double* sink, int dep) {
     uint64_t a0 = threadIdx.x, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4, a5 = a0 + 5, a6 = a0 + 6, a7 = a0 + 7;
@@ -143,7 +185,23 @@ int main() {
                     {"v_cmp_gt_u32 vcc + v_cndmask_b32 (pair)", k_cndmask_vcmp}, {"v_cmp_gt_f32 vcc", k_cmp_f32},
                     {"v_mov_b32", k_mov},              {"v_xor_b32", k_xor32},
                     {"v_max_f32", k_max_f32},          {"v_med3_f32", k_med3_f32},
-                    {"v_lshlrev_b32", k_lshl_b32},     {"v_bfi_b32", k_bfi}};
+                    {"v_lshlrev_b32", k_lshl_b32},     {"v_bfi_b32", k_bfi},
+                    {"v_add3_u32", k_add3},            {"v_lshl_add_u32", k_lshl_add_u32},
+                    {"v_mbcnt_lo_u32_b32", k_mbcnt},   {"v_rcp_f32", k_rcp_f32},
+                    {"v_rcp_f64", k_rcp_f64},          {"v_ldexp_f64", k_ldexp_f64},
+                    {"v_bfrev_b32", k_bfrev},          {"v_and_or_b32", k_and_or},
+                    {"v_not_b32", k_not32},            {"v_add_co_u32", k_add_co},
+                    {"v_mov_b64", k_mov_b64},          {"v_max_f64", k_max_f64},
+                    {"v_cmp_lt_f64 vcc", k_cmp_f64},   {"v_cmp_gt_u64 vcc", k_cmp_u64},
+                    {"v_lshrrev_b32", k_lshr_b32},     {"v_and_b32", k_and32},
+                    {"v_lshlrev_b64", k_lshl_b64},     {"v_mul_f32", k_mul_f32},
+                    {"v_sub_u32", k_sub_u32},
+                    {"v_max_i32", k_max_i32},          {"v_min_i32", k_min_i32},
+                    {"v_max3_i32", k_max3_i32},        {"v_min3_i32", k_min3_i32},
+                    {"v_max_u32", k_max_u32},          {"v_cmp_le_i32 vcc", k_cmp_le_i32},
+                    {"v_maximum3_f32", k_maximum3_f32}, {"v_min_f32", k_min_f32},
+                    {"v_sub_f32", k_sub_f32},          {"v_pk_add_f32", k_pk_add_f32},
+                    {"v_ashrrev_i32", k_ashr_i32}};
     int cus = 0;
     CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
     unsigned long long* d_cyc = nullptr;
