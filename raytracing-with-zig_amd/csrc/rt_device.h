@@ -91,7 +91,9 @@ struct RayDiv {
         const bool far = !(hi2 - (423u << 21) < (1200u << 21));
         // rare: wave-uniform test, see uniform().  The per-ray part is the mask `bad`, OR-ed on the
         // scalar unit; folding it into the per-lane bool made the compiler materialize that bool
-        // with two VALU ops per division.
+        // with two VALU ops per division.  (Round 4: the range test as two f64 |x| compares into
+        // lane masks plus an inverse ballot cut walk_setup's static VALU cycles by 11% and made the
+        // frame 1.5% slower: a longer scalar chain ahead of the branch, profiles/r04_range_ab/.)
         if (__builtin_expect((__ballot(far) | bad) != 0, 0)) {
             RTK_MARK("rare");
             if (far || ((bad >> lane()) & 1)) q = x / a;
@@ -154,6 +156,11 @@ __device__ __forceinline__ v3 refract(v3 v, v3 n, double eta) {
 // DefaultPrng.init, from the key rt_sample_key(seed, pixel, sample) — counter-based, so any
 // partition of the image over lanes/GPUs draws the same numbers.
 // ------------------------------------------------------------------------------------------------
+// A/B knob for the draw's instruction forms (0: rounds 1-3; 1: the 64-bit shift `s1 << 17` as one
+// v_lshlrev_b64 — config 4 -0.74%, rank 0 of 8 -0.77%, bit-identical, profiles/r04_rng_ab/)
+#ifndef RTZIG_RNG_FORM
+#define RTZIG_RNG_FORM 1
+#endif
 __device__ __forceinline__ uint64_t rotl64(uint64_t x, int k) { return (x << k) | (x >> (64 - k)); }
 // rotl64 by a constant K as two v_alignbit_b32 (the compiler's form is a 64-bit shift, a 32-bit
 // shift and an or): for K < 32 the high word is alignbit(hi, lo, 32 - K), the low word
@@ -220,7 +227,14 @@ struct Rng {
     // ops per draw instead of 12
     __device__ __forceinline__ uint64_t next() {
         const uint64_t r = rotl64c<23>(s0 + s3) + s0;
+#if RTZIG_RNG_FORM == 1
+        // one v_lshlrev_b64 (2.1 SIMD cycles at 4 waves/SIMD): left alone the compiler splits the
+        // shift into v_alignbit_b32 + v_lshlrev_b32 (3.1 + 3.0) for the 32-bit xors that consume it
+        uint64_t t;
+        asm("v_lshlrev_b64 %0, 17, %1" : "=v"(t) : "v"(s1));
+#else
         const uint64_t t = s1 << 17;
+#endif
         const uint64_t n1 = xor3_64(s1, s2, s0);
         const uint64_t n0 = xor3_64(s0, s3, s1);
         const uint64_t n2 = xor3_64(s2, s0, t);

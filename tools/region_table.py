@@ -50,6 +50,8 @@ def load_rates(path=RATES):
     out = {}
     for r in json.load(open(path))["results"]:
         op = r["op"].split()[0]
+        if "(pair)" in r["op"]:  # a cmp + cndmask pair, not one opcode
+            continue
         if op == "v_cndmask_b32":  # VOP2 form reading a VCC nothing wrote: an artifact (README); use the e64 rate
             continue
         out[op] = r["simd_cycles_per_instr_4waves"]
