@@ -157,9 +157,11 @@ __device__ __forceinline__ v3 refract(v3 v, v3 n, double eta) {
 // partition of the image over lanes/GPUs draws the same numbers.
 // ------------------------------------------------------------------------------------------------
 // A/B knob for the draw's instruction forms (0: rounds 1-3; 1: the 64-bit shift `s1 << 17` as one
-// v_lshlrev_b64 — config 4 -0.74%, rank 0 of 8 -0.77%, bit-identical, profiles/r04_rng_ab/)
+// v_lshlrev_b64 — config 4 -0.74%, rank 0 of 8 -0.77%; 2: also Random.float's bit select as
+// v_bitop3_b32 instead of v_bfi_b32 — a further -0.2% on config 4, within noise, fewer issue cycles;
+// all bit-identical, profiles/r04_rng_ab/)
 #ifndef RTZIG_RNG_FORM
-#define RTZIG_RNG_FORM 1
+#define RTZIG_RNG_FORM 2
 #endif
 __device__ __forceinline__ uint64_t rotl64(uint64_t x, int k) { return (x << k) | (x >> (64 - k)); }
 // rotl64 by a constant K as two v_alignbit_b32 (the compiler's form is a 64-bit shift, a 32-bit
@@ -227,7 +229,7 @@ struct Rng {
     // ops per draw instead of 12
     __device__ __forceinline__ uint64_t next() {
         const uint64_t r = rotl64c<23>(s0 + s3) + s0;
-#if RTZIG_RNG_FORM == 1
+#if RTZIG_RNG_FORM >= 1
         // one v_lshlrev_b64 (2.1 SIMD cycles at 4 waves/SIMD): left alone the compiler splits the
         // shift into v_alignbit_b32 + v_lshlrev_b32 (3.1 + 3.0) for the 32-bit xors that consume it
         uint64_t t;
@@ -257,7 +259,13 @@ struct Rng {
         // (VOP3 takes no literals and one SGPR: the 1022 << 20 addend lives in a VGPR)
         uint32_t e, ohi;
         asm("v_mad_i32_i24 %0, %1, %2, %3" : "=v"(e) : "v"((uint32_t)__builtin_clz(hi)), "s"(-(1 << 20)), "v"(1022u << 20));
+#if RTZIG_RNG_FORM >= 2
+        // the same bit select as v_bitop3_b32 (1.9 SIMD cycles against v_bfi_b32's 3.1): truth table
+        // 0xe4 = S2 ? S0 : S1 per bit, the mask in S2 (the form LLVM emits for a variable mask)
+        asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xe4" : "=v"(ohi) : "v"(hi), "v"(e), "s"(0xfffffu));
+#else
         asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(ohi) : "s"(0xfffffu), "v"(hi), "v"(e));
+#endif
         double res = __builtin_bit_cast(double, u32x2{(uint32_t)rnd, ohi});
         // >= 12 leading zeros (p = 2^-12 per draw): the fast result is computed for every lane and
         // the rare lanes are redone, behind a wave-uniform test so the common case has no
