@@ -262,14 +262,23 @@ def run(args):
         buf = outs[b]
         if freed[b] is not None:
             stream.wait_event(freed[b])  # the gather that last read this buffer has finished
+        if stream is coll:
+            if n_rows:
+                renderer.render_rows_async(cam.cam, buf.data_ptr(), row0=row0, row_step=step,
+                                           n_rows=n_rows, output=args.output, d_stats_ptr=stats_ptr,
+                                           stream_ptr=stream.cuda_stream)
+            return gather(buf)
         if n_rows:
+            # the output is completed on the collective stream (rt_render_rows_async_split): the
+            # sample kernel runs on the render stream and a direct-mode launch's reduce pass on the
+            # collective stream, ahead of this frame's gather, so it overlaps the next frame's
+            # sample kernel (rank 0 of 8 on config 4: -1.5%, profiles/r04_split_ab/)
             renderer.render_rows_async(cam.cam, buf.data_ptr(), row0=row0, row_step=step,
                                        n_rows=n_rows, output=args.output, d_stats_ptr=stats_ptr,
-                                       stream_ptr=stream.cuda_stream)
-        if stream is coll:
-            return gather(buf)
-        rendered[b].record(stream)
-        coll.wait_event(rendered[b])
+                                       stream_ptr=stream.cuda_stream, out_stream_ptr=coll.cuda_stream)
+        else:
+            rendered[b].record(stream)
+            coll.wait_event(rendered[b])
         img = gather(buf)
         freed[b] = torch.cuda.Event()
         freed[b].record(coll)
@@ -431,7 +440,8 @@ def run(args):
                            + ((", RCCL gather to rank 0" if args.dist_backend == "nccl" else
                                ", gloo gather to rank 0 (rehearsal: ranks share devices)")
                               + (" (1-rank group, --collective)" if world == 1 else "")
-                              + ", each frame's gather overlapped with the next frame's render (two row buffers)"
+                              + ", each frame's gather (and a direct-mode reduce pass) overlapped with the next "
+                                "frame's render (two row buffers)"
                               if grouped else "")},
             "roofline": {
                 "bound": "valu",

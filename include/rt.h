@@ -151,6 +151,18 @@ int rt_context_set_scene(rt_context* ctx, const rt_sphere* spheres, size_t n_sph
 int rt_render_rows_async(rt_context* ctx, const rt_camera* cam, uint32_t output_format,
                          uint32_t row0, uint32_t row_step, uint32_t n_rows,
                          void* d_out, void* d_stats, void* stream);
+/* The same render with the output completed on a second stream `out_stream` instead of `stream`
+ * (frame pipelining for multi-frame drivers, e.g. bench.py's N > 1 path, which gathers each frame
+ * on its collective stream): the sample kernel runs on `stream`; `out_stream` waits for it, and a
+ * direct-mode call (small launches: a rank's rows of a multi-GPU job) runs its reduce pass there.
+ * The context then alternates two per-sample buffers, so the next call's sample kernel on `stream`
+ * does not wait for this call's reduce pass — the pass (HBM-bound, ≈0.25 ms at rank 0 of 8 on
+ * config 4) overlaps the next sample kernel.  The output, and `d_stats`, are complete when
+ * `out_stream` reaches the point of the call.  out_stream == NULL or == stream: rt_render_rows_async.
+ * Workspace: twice direct mode's per-sample buffer. */
+int rt_render_rows_async_split(rt_context* ctx, const rt_camera* cam, uint32_t output_format,
+                               uint32_t row0, uint32_t row_step, uint32_t n_rows,
+                               void* d_out, void* d_stats, void* stream, void* out_stream);
 /* Waits for the context's last render and reports a failure the kernel recorded (RT_ERR_HIP: a
  * wave gave up waiting for a running-sum hand-off — a bug guard, never expected). */
 int rt_context_sync(rt_context* ctx);
@@ -165,7 +177,8 @@ int rt_context_workspace_bytes(rt_context* ctx, uint64_t* bytes);
 /* Optional kernel timing with HIP events recorded on the launch stream around the kernels of every
  * render call.  rt_context_kernel_times waits for the last event and returns the durations (ms) of
  * the most recent rt_render_rows_async call: the sample kernel, and the reduce pass of direct mode
- * (small launches, see rt_render; ~0 when the sample kernel accumulated in order itself). */
+ * (small launches, see rt_render; ~0 when the sample kernel accumulated in order itself; for a split
+ * call, from the point `out_stream` reaches the pass to its end). */
 int rt_context_enable_timing(rt_context* ctx, int enable);
 int rt_context_kernel_times(rt_context* ctx, double* sample_ms, double* reduce_ms);
 /* The same summed over every call since timing was (re)enabled (at most 1024 calls; beyond that the

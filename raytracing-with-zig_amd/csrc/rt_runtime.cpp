@@ -42,6 +42,7 @@ void rt_set_last_error(const std::string& msg);
 namespace {
 
 constexpr uint32_t kMaxTimed = 1024;  // event-pool bound of rt_context_kernel_times_total
+constexpr size_t kEventsPerCall = 4;   // timed call: start, sample kernel done, reduce start, reduce done
 
 // Host-side scene: device records of the Hittable list plus its BVH, built once per sphere list and
 // uploaded to every device that renders it.
@@ -95,6 +96,11 @@ struct rt_context {
     size_t flags_bytes = 0;
     double* d_samples = nullptr;    // direct mode: [spp][P][3] (at most rtk::kDirectBytes)
     size_t samples_bytes = 0;
+    double* d_samples2 = nullptr;   // the second per-sample buffer of split calls (rt_render_rows_async_split)
+    size_t samples2_bytes = 0;
+    uint32_t samples_flip = 0;      // the buffer the next split call's samples go to
+    hipEvent_t reduced[2] = {nullptr, nullptr};  // the last reduce pass that read buffer 0 / 1 has ended
+    bool reduced_valid[2] = {false, false};
     std::vector<uint32_t> sched;    // chunk table of the last launch (rt_schedule.hpp), and its copy
     uint32_t* d_sched = nullptr;
     size_t sched_bytes = 0;
@@ -108,11 +114,16 @@ struct rt_context {
     rtk::GeoRec* d_always_geo = nullptr;
     uint32_t* d_always_sid = nullptr;
     size_t nodes_bytes = 0, leaves_bytes = 0, always_geo_bytes = 0, always_sid_bytes = 0;
-    // ordering: `done` is recorded on the caller's stream after the launch of a render call; device
-    // buffers are only rewritten after it (quiesce), and a render on another stream first waits for it
+    // ordering: `done` is recorded after the last operation of a render call (the reduce pass of a
+    // split call: on its out stream, which waited for the sample kernel); device buffers are only
+    // rewritten after it (quiesce).  `launched` is recorded on the launch stream after the sample
+    // kernel: a render on another stream first waits for it, and a render that writes a per-sample
+    // buffer waits for the reduce pass that last read it (`reduced`).
     hipEvent_t done = nullptr;
     bool done_valid = false;
-    hipStream_t done_stream = nullptr;
+    hipEvent_t launched = nullptr;
+    bool launched_valid = false;
+    hipStream_t launched_stream = nullptr;
     // optional kernel timing: an event pair around every launch
     bool timing = false;
     bool profile = false;  // instrumented kernels: d_stats must hold RT_PROFILE_STATS_WORDS uint64 (rt.h)
@@ -626,6 +637,9 @@ int rt_context_create(int device, rt_context** out_ctx) {
     ctx->device = device;
     hipError_t e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = make_event(&ctx->done, false);
+    if (e == hipSuccess) e = make_event(&ctx->launched, false);
+    if (e == hipSuccess) e = make_event(&ctx->reduced[0], false);
+    if (e == hipSuccess) e = make_event(&ctx->reduced[1], false);
     int cus = 0;
     if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
     ctx->sched_lanes = (uint64_t)std::max(cus, 1) * 16 * 64;
@@ -644,13 +658,14 @@ int rt_context_destroy(rt_context* ctx) {
     if (ctx->done_valid) (void)hipEventSynchronize(ctx->done);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     for (void* p : {(void*)ctx->d_geo, (void*)ctx->d_mat, (void*)ctx->d_ring, (void*)ctx->d_sums, (void*)ctx->d_flags,
-                    (void*)ctx->d_samples, (void*)ctx->d_sched, (void*)ctx->d_ctr, (void*)ctx->d_nodes, (void*)ctx->d_leaves, (void*)ctx->d_always_geo,
+                    (void*)ctx->d_samples, (void*)ctx->d_samples2, (void*)ctx->d_sched, (void*)ctx->d_ctr, (void*)ctx->d_nodes, (void*)ctx->d_leaves, (void*)ctx->d_always_geo,
                     (void*)ctx->d_always_sid, ctx->d_out, (void*)ctx->d_stats})
         (void)hipFree(p);
     if (ctx->h_out) (void)hipHostFree(ctx->h_out);
     if (ctx->h_stats) (void)hipHostFree(ctx->h_stats);
     for (hipEvent_t e : ctx->events) (void)hipEventDestroy(e);
-    if (ctx->done) (void)hipEventDestroy(ctx->done);
+    for (hipEvent_t e : {ctx->done, ctx->launched, ctx->reduced[0], ctx->reduced[1]})
+        if (e) (void)hipEventDestroy(e);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
     return RT_OK;
@@ -686,8 +701,16 @@ int rt_context_sync(rt_context* ctx) {
     return RT_OK;
 }
 
-int rt_render_rows_async(rt_context* ctx, const rt_camera* cam, uint32_t output_format, uint32_t row0,
-                         uint32_t row_step, uint32_t n_rows, void* d_out, void* d_stats, void* stream) {
+}  // extern "C"
+
+namespace {
+
+// One render call.  os == nullptr: everything on s (rt_render_rows_async).  Otherwise the output is
+// completed in os's order: direct mode's reduce pass runs on os after the sample kernel on s, over
+// one of two per-sample buffers taken in turn, so the next call's sample kernel on s need not wait
+// for this call's reduce pass (rt_render_rows_async_split).
+int render_rows(rt_context* ctx, const rt_camera* cam, uint32_t output_format, uint32_t row0, uint32_t row_step,
+                uint32_t n_rows, void* d_out, void* d_stats, hipStream_t s, hipStream_t os) {
     if (!ctx) { rt_set_last_error("null context"); return RT_ERR_INVALID; }
     int rc = validate_camera(cam);
     if (rc) return rc;
@@ -702,7 +725,7 @@ int rt_render_rows_async(rt_context* ctx, const rt_camera* cam, uint32_t output_
         return RT_ERR_INVALID;
     }
     HIP_CHECK(hipSetDevice(ctx->device));
-    hipStream_t s = (hipStream_t)stream;  // NULL = the HIP null stream, like torch's default stream
+    if (os == s) os = nullptr;  // one stream: the plain call
 
     // camera-ray origins (center + defocus disk) must lie inside the BVH padding's origin bound
     // (lanes outside it would walk without culling: correct, but every camera ray would pay)
@@ -768,12 +791,23 @@ int rt_render_rows_async(rt_context* ctx, const rt_camera* cam, uint32_t output_
                                           direct, plan_waves);
         return rtk_launch_samples(&p, ctx->d_geo, ctx->d_mat, u, d_stats, s, &ctx->last_kernel, direct, plan_waves);
     };
-    // a context holds the workspace of one mode at a time (rt.h "Workspace")
+    // a context holds the workspace of one mode at a time (rt.h "Workspace"); split calls in direct
+    // mode alternate two per-sample buffers
+    const bool split_reduce = direct && os != nullptr;
+    uint32_t sbuf = 0;
     if (direct) {
         rc = release_buffer(ctx, (void**)&ctx->d_ring, &ctx->ring_bytes);
         if (!rc) rc = release_buffer(ctx, (void**)&ctx->d_sums, &ctx->sums_bytes);
         ctx->ring_waves = 0;
         if (!rc) rc = fit_buffer(ctx, (void**)&ctx->d_samples, &ctx->samples_bytes, direct_bytes);
+        if (split_reduce) {
+            if (!rc) rc = fit_buffer(ctx, (void**)&ctx->d_samples2, &ctx->samples2_bytes, direct_bytes);
+            sbuf = ctx->samples_flip;
+            ctx->samples_flip ^= 1u;
+        } else {
+            if (!rc) rc = release_buffer(ctx, (void**)&ctx->d_samples2, &ctx->samples2_bytes);
+            ctx->samples_flip = 0;
+        }
     } else {
         // the ring holds the persistent grid of the kernel this call launches (its resident waves)
         uint32_t waves = 0;
@@ -781,6 +815,8 @@ int rt_render_rows_async(rt_context* ctx, const rt_camera* cam, uint32_t output_
         waves = std::max(waves, 1u);
         constexpr size_t kWaveBytes = rtk::kRingWaveDoubles * sizeof(double);
         rc = release_buffer(ctx, (void**)&ctx->d_samples, &ctx->samples_bytes);
+        if (!rc) rc = release_buffer(ctx, (void**)&ctx->d_samples2, &ctx->samples2_bytes);
+        ctx->samples_flip = 0;
         if (!rc) rc = fit_buffer(ctx, (void**)&ctx->d_ring, &ctx->ring_bytes, (size_t)waves * kWaveBytes);
         ctx->ring_waves = rc ? 0u : (uint32_t)(ctx->ring_bytes / kWaveBytes);
         if (!rc && ua.n_chunks > 1) rc = fit_buffer(ctx, (void**)&ctx->d_sums, &ctx->sums_bytes, P * 3 * sizeof(double));
@@ -798,7 +834,7 @@ int rt_render_rows_async(rt_context* ctx, const rt_camera* cam, uint32_t output_
     if (rc) return rc;
     ua.ring = direct ? nullptr : ctx->d_ring;
     ua.sums = direct ? nullptr : ctx->d_sums;
-    ua.samples = direct ? ctx->d_samples : nullptr;
+    ua.samples = direct ? (sbuf ? ctx->d_samples2 : ctx->d_samples) : nullptr;
     ua.spp = cam->samples_per_pixel;
     ua.flags = ctx->d_flags;
     ua.out = d_out;
@@ -823,27 +859,60 @@ int rt_render_rows_async(rt_context* ctx, const rt_camera* cam, uint32_t output_
         if (ctx->log_used + 1 > kMaxTimed) ctx->log_used = 0;  // wrap: totals restart
         ctx->call_first = ctx->log_used;
         ctx->log_used += 1;
-        while (ctx->events.size() < 3 * (size_t)ctx->log_used) {
+        while (ctx->events.size() < kEventsPerCall * (size_t)ctx->log_used) {
             hipEvent_t e;
             HIP_CHECK(make_event(&e, true));
             ctx->events.push_back(e);
         }
         ctx->timed_calls = 1;
     }
-    // a previous render of this context on another stream may still use the buffers
-    if (ctx->done_valid && ctx->done_stream != s) HIP_CHECK(hipStreamWaitEvent(s, ctx->done, 0));
+    // a previous render of this context's on another stream may still run its sample kernel (the
+    // counters, flags, ring and sums are the sample kernel's own); the per-sample buffer this call
+    // writes may still be read by the reduce pass of an earlier call (on any stream)
+    if (ctx->launched_valid && ctx->launched_stream != s) HIP_CHECK(hipStreamWaitEvent(s, ctx->launched, 0));
+    if (direct && ctx->reduced_valid[sbuf]) HIP_CHECK(hipStreamWaitEvent(s, ctx->reduced[sbuf], 0));
     HIP_CHECK(hipMemsetAsync(ctx->d_ctr, 0, rtk::kCtrLaunchBytes, s));  // not the sticky error word
     if (!direct) HIP_CHECK(hipMemsetAsync(ctx->d_flags, 0, flag_bytes, s));
-    hipEvent_t* ev = ctx->timing ? &ctx->events[3 * ctx->call_first] : nullptr;
+    hipEvent_t* ev = ctx->timing ? &ctx->events[kEventsPerCall * ctx->call_first] : nullptr;
     if (ev) HIP_CHECK(hipEventRecord(ev[0], s));
     HIP_CHECK(launch(&ua, nullptr));
     if (ev) HIP_CHECK(hipEventRecord(ev[1], s));
-    if (direct) HIP_CHECK(rtk_launch_reduce(&ua, s));
-    if (ev) HIP_CHECK(hipEventRecord(ev[2], s));
-    HIP_CHECK(hipEventRecord(ctx->done, s));
+    HIP_CHECK(hipEventRecord(ctx->launched, s));
+    ctx->launched_valid = true;
+    ctx->launched_stream = s;
+    // the stream on which the output is complete: split calls continue on os, after the sample kernel
+    hipStream_t rs = s;
+    if (os) {
+        HIP_CHECK(hipStreamWaitEvent(os, ctx->launched, 0));
+        rs = os;
+    }
+    if (ev) HIP_CHECK(hipEventRecord(ev[2], rs));
+    if (direct) {
+        HIP_CHECK(rtk_launch_reduce(&ua, rs));
+        HIP_CHECK(hipEventRecord(ctx->reduced[sbuf], rs));
+        ctx->reduced_valid[sbuf] = true;
+    }
+    if (ev) HIP_CHECK(hipEventRecord(ev[3], rs));
+    HIP_CHECK(hipEventRecord(ctx->done, rs));
     ctx->done_valid = true;
-    ctx->done_stream = s;
     return RT_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int rt_render_rows_async(rt_context* ctx, const rt_camera* cam, uint32_t output_format, uint32_t row0,
+                         uint32_t row_step, uint32_t n_rows, void* d_out, void* d_stats, void* stream) {
+    // NULL = the HIP null stream, like torch's default stream
+    return render_rows(ctx, cam, output_format, row0, row_step, n_rows, d_out, d_stats, (hipStream_t)stream, nullptr);
+}
+
+int rt_render_rows_async_split(rt_context* ctx, const rt_camera* cam, uint32_t output_format, uint32_t row0,
+                               uint32_t row_step, uint32_t n_rows, void* d_out, void* d_stats, void* stream,
+                               void* out_stream) {
+    return render_rows(ctx, cam, output_format, row0, row_step, n_rows, d_out, d_stats, (hipStream_t)stream,
+                       (hipStream_t)out_stream);
 }
 
 int rt_context_enable_timing(rt_context* ctx, int enable) {
@@ -876,9 +945,10 @@ static int sum_times(rt_context* ctx, uint32_t first, uint32_t count, double* sa
     double sm = 0, rm = 0;
     for (uint32_t c = first; c < first + count; c++) {
         float a = 0, b = 0;
-        HIP_CHECK(hipEventSynchronize(ctx->events[3 * c + 2]));
-        HIP_CHECK(hipEventElapsedTime(&a, ctx->events[3 * c + 0], ctx->events[3 * c + 1]));
-        HIP_CHECK(hipEventElapsedTime(&b, ctx->events[3 * c + 1], ctx->events[3 * c + 2]));
+        const hipEvent_t* e = &ctx->events[kEventsPerCall * c];  // start, sample kernel done, reduce start, end
+        HIP_CHECK(hipEventSynchronize(e[3]));
+        HIP_CHECK(hipEventElapsedTime(&a, e[0], e[1]));
+        HIP_CHECK(hipEventElapsedTime(&b, e[2], e[3]));
         sm += a;
         rm += b;
     }
@@ -906,7 +976,8 @@ const char* rt_kernel_name(rt_context* ctx) { return ctx ? ctx->last_kernel : "r
 
 int rt_context_workspace_bytes(rt_context* ctx, uint64_t* bytes) {
     if (!ctx || !bytes) { rt_set_last_error("null context / output"); return RT_ERR_INVALID; }
-    *bytes = (uint64_t)ctx->ring_bytes + ctx->sums_bytes + ctx->flags_bytes + ctx->samples_bytes + ctx->sched_bytes +
+    *bytes = (uint64_t)ctx->ring_bytes + ctx->sums_bytes + ctx->flags_bytes + ctx->samples_bytes + ctx->samples2_bytes +
+             ctx->sched_bytes +
              (ctx->d_ctr ? rtk::kCtrBytes : 0);
     return RT_OK;
 }

@@ -192,10 +192,19 @@ class DeviceRenderer:
         check("rt_context_set_scene", self.lib.rt_context_set_scene(self.ctx, spheres, n))
 
     def render_rows_async(self, cam, d_out_ptr, row0=0, row_step=1, n_rows=None, output="linear",
-                          d_stats_ptr=None, stream_ptr=None):
+                          d_stats_ptr=None, stream_ptr=None, out_stream_ptr=None):
+        """out_stream_ptr: complete the output on that stream instead (rt_render_rows_async_split:
+        direct mode's reduce pass runs there, over two per-sample buffers taken in turn, so it
+        overlaps the next call's sample kernel on stream_ptr)."""
         if n_rows is None:
             n_rows = (cam.image_height - row0 + row_step - 1) // row_step
         fmt = abi.RT_OUT_LINEAR_F64 if output == "linear" else abi.RT_OUT_RGB8
+        if out_stream_ptr:
+            check("rt_render_rows_async_split",
+                  self.lib.rt_render_rows_async_split(self.ctx, C.byref(cam), fmt, row0, row_step, n_rows,
+                                                      C.c_void_p(d_out_ptr), C.c_void_p(d_stats_ptr or 0),
+                                                      C.c_void_p(stream_ptr or 0), C.c_void_p(out_stream_ptr)))
+            return
         check("rt_render_rows_async",
               self.lib.rt_render_rows_async(self.ctx, C.byref(cam), fmt, row0, row_step, n_rows,
                                             C.c_void_p(d_out_ptr), C.c_void_p(d_stats_ptr or 0),

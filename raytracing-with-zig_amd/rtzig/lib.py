@@ -18,6 +18,7 @@ EXPORTED = [
     "rt_context_destroy",
     "rt_context_set_scene",
     "rt_render_rows_async",
+    "rt_render_rows_async_split",
     "rt_kernel_name",
     "rt_context_workspace_bytes",
     "rt_context_enable_timing",
@@ -62,6 +63,8 @@ def _declare(lib):
         "rt_context_set_scene": (C.c_int, [vp, P(RtSphere), C.c_size_t]),
         "rt_render_rows_async": (C.c_int, [vp, P(RtCamera), C.c_uint32, C.c_uint32, C.c_uint32,
                                            C.c_uint32, vp, vp, vp]),
+        "rt_render_rows_async_split": (C.c_int, [vp, P(RtCamera), C.c_uint32, C.c_uint32, C.c_uint32,
+                                                 C.c_uint32, vp, vp, vp, vp]),
         "rt_kernel_name": (C.c_char_p, [vp]),
         "rt_context_workspace_bytes": (C.c_int, [vp, P(C.c_uint64)]),
         "rt_context_enable_timing": (C.c_int, [vp, C.c_int]),

@@ -633,3 +633,45 @@ def test_direct_rows_instrumented_bit_exact(oracle, profile, monkeypatch):
     st = stats.cpu().tolist()
     assert np.array_equal(out.cpu().numpy(), ref)
     assert st[0] == rays and st[1] == 12 * 1200 * 24
+
+
+@pytest.mark.parametrize("mode", ["direct", "ring"])
+def test_split_render_pipeline_bit_exact(oracle, mode, monkeypatch):
+    """rt_render_rows_async_split (bench.py's N > 1 frame pipeline): the sample kernel on one stream,
+    the output completed on a second one (direct mode: the reduce pass there, over two per-sample
+    buffers taken in turn).  Four frames back to back into two row buffers, each consumed on the
+    second stream, interleaved with a plain call: every frame bit-exact against oracle B with exact
+    sample counts, and direct mode holds two per-sample buffers (reference: the row loop
+    camera.zig:128-138 that a rank's launch replaces)."""
+    import torch
+    monkeypatch.setenv("RTZIG_UNIT_MODE", mode)
+    cam = rtzig.final_scene_camera(width=1200, aspect_ratio=1.5, spp=24)
+    ref, rays = oracle.render_b(cam.cam, cam.scene.world, row0=5, row_step=8, n_rows=12, threads=16)
+    r = rtzig.DeviceRenderer(0)
+    r.set_scene(cam.scene.world)
+    render, coll = torch.cuda.Stream(), torch.cuda.Stream()
+    outs = [torch.zeros((12, 1200, 3), dtype=torch.float64, device="cuda:0") for _ in range(2)]
+    stats = torch.zeros(2, dtype=torch.int64, device="cuda:0")
+    got = []
+    for k in range(4):
+        buf = outs[k % 2]
+        r.render_rows_async(cam.cam, buf.data_ptr(), row0=5, row_step=8, n_rows=12, d_stats_ptr=stats.data_ptr(),
+                            stream_ptr=render.cuda_stream, out_stream_ptr=coll.cuda_stream)
+        with torch.cuda.stream(coll):
+            got.append(buf.clone())  # ordered after this frame's output on the second stream
+        render.wait_stream(coll)  # the next frame into this buffer only after the copy
+        if k == 1:
+            direct_ws = r.workspace_bytes()
+    plain = torch.zeros_like(outs[0])
+    r.render_rows_async(cam.cam, plain.data_ptr(), row0=5, row_step=8, n_rows=12, stream_ptr=render.cuda_stream)
+    torch.cuda.synchronize()
+    r.sync()
+    assert ("direct" in r.kernel_name()) == (mode == "direct")
+    per_buf = 24 * 1200 * 12 * 24  # spp x pixels x 24 B
+    if mode == "direct":
+        assert direct_ws >= 2 * per_buf
+    r.close()
+    for img in got + [plain]:
+        assert np.array_equal(img.cpu().numpy(), ref)
+    st = stats.cpu().tolist()
+    assert st[1] == 4 * 12 * 1200 * 24 and st[0] == 4 * rays

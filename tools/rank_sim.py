@@ -39,6 +39,10 @@ ap.add_argument("--reps", type=int, default=3)
 ap.add_argument("--width", type=int, default=1200)
 ap.add_argument("--aspect", type=float, default=1.5)
 ap.add_argument("--ns", type=int, nargs="+", default=[1, 2, 4, 8])
+ap.add_argument("--pipe-frames", type=int, default=0,
+                help="also time each rank's rows in bench.py's frame pipeline (two row buffers, render "
+                     "stream, output completed on a second stream: rt_render_rows_async_split), this many "
+                     "frames, wall clock per frame")
 args = ap.parse_args()
 
 cam = rtzig.final_scene_camera(width=args.width, aspect_ratio=args.aspect, spp=args.spp)
@@ -58,15 +62,50 @@ def kernel_ms(row0, step, n_rows):
     return min(ks)
 
 
+def pipeline_ms(row0, step, n_rows):
+    """bench.py's N > 1 loop without the collective: frame k renders into buffer k % 2 on the render
+    stream with its output (direct mode: the reduce pass) completed on the second stream, where the
+    gather would run; wall clock per frame over args.pipe_frames frames."""
+    render, coll = torch.cuda.Stream(), torch.cuda.Stream()
+    outs = [torch.empty((n_rows, W, 3), dtype=torch.float64, device="cuda:0") for _ in range(2)]
+    freed = [None, None]
+
+    def frame(k):
+        b = k % 2
+        if freed[b] is not None:
+            render.wait_event(freed[b])
+        r.render_rows_async(cam.cam, outs[b].data_ptr(), row0=row0, row_step=step, n_rows=n_rows,
+                            stream_ptr=render.cuda_stream, out_stream_ptr=coll.cuda_stream)
+        freed[b] = torch.cuda.Event()
+        freed[b].record(coll)
+
+    for k in range(2):
+        frame(k)
+    torch.cuda.synchronize()
+    best = None
+    for _ in range(args.reps):
+        t0 = time.perf_counter()
+        for k in range(args.pipe_frames):
+            frame(k)
+        torch.cuda.synchronize()
+        ms = (time.perf_counter() - t0) / args.pipe_frames * 1e3
+        best = ms if best is None else min(best, ms)
+    return best
+
+
 res = {"config": f"{W}x{H} {args.spp}spp", "link_GBps_model": LINK_GBPS, "launch_us_model": LAUNCH_US, "ranks": {}}
 base = None
+pipe_base = None
 for n in args.ns:
     R = rdist.rows_per_rank(H, n)
-    per_rank = []
+    per_rank, per_rank_pipe = [], []
     for rank in range(n):
         row0, step, n_rows = rdist.rank_rows(H, rank, n)
         per_rank.append(kernel_ms(row0, step, n_rows))
-        print(f"N={n} rank {rank}: {per_rank[-1]:.3f} ms", file=sys.stderr, flush=True)
+        if args.pipe_frames:
+            per_rank_pipe.append(pipeline_ms(row0, step, n_rows))
+        print(f"N={n} rank {rank}: {per_rank[-1]:.3f} ms" +
+              (f", pipelined {per_rank_pipe[-1]:.3f} ms per frame" if per_rank_pipe else ""), file=sys.stderr, flush=True)
     k = max(per_rank)
     gather = 0.0
     if n > 1:
@@ -92,4 +131,12 @@ for n in args.ns:
                        "efficiency": round(base / frame / n, 3),
                        "frame_ms_gather_overlapped": round(frame_ovl, 3),
                        "efficiency_gather_overlapped": round(base / frame_ovl / n, 3)}
+    if per_rank_pipe:
+        # the steady-state frame of the pipeline (gather hidden beside the next render, reduce pass on
+        # the second stream), max over ranks, against the 1-rank pipeline's frame
+        pf = max(max(per_rank_pipe), gather)
+        pipe_base = pipe_base or pf
+        res["ranks"][n].update({"pipelined_frame_ms_max_over_ranks": round(max(per_rank_pipe), 3),
+                                "pipelined_frame_ms_min_over_ranks": round(min(per_rank_pipe), 3),
+                                "efficiency_pipelined": round(pipe_base / pf / n, 3)})
 print(json.dumps(res))
