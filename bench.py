@@ -145,6 +145,11 @@ def parse_args(argv=None):
                     help="at --gpus 1, still join a (1-rank) process group on --dist-backend and run the "
                          "N>1 pipeline: two row buffers, the render stream, and each frame's dist.gather on "
                          "the collective stream (nccl: the RCCL gather on one GPU)")
+    ap.add_argument("--pipeline", choices=["split", "deferred"], default="split",
+                    help="N > 1 frame loop: 'split' completes each frame's output on the collective stream "
+                         "(rt_render_rows_async_split); 'deferred' also leaves a direct-mode frame's reduce "
+                         "pass to the next frame's drained waves (rt_render_rows_async_deferred), gathering "
+                         "each frame once the next one is issued")
     ap.add_argument("--launch-check", action="store_true",
                     help="start the ranks and join the process group, print one line, render nothing")
     return ap.parse_args(argv)
@@ -256,7 +261,53 @@ def run(args):
             return rdist.gather_image(buf.cpu(), H, rank, world, collective=grouped)  # gloo: host tensors
         return rdist.gather_image(buf, H, rank, world, collective=grouped)
 
+    pend = [False]  # the last deferred frame's output is still pending (its reduce pass not yet run)
+
+    def frame_deferred(stats_ptr=None):
+        # rt_render_rows_async_deferred: frame j's kernel folds frame j-1's reduce pass into its row
+        # buffer in the launch's tail, so frame j-1 is gathered after frame j is issued; a ring-mode
+        # frame (nothing pending) is gathered at once, as with the split call
+        j = nframe[0]
+        nframe[0] += 1
+        b, pb = j % 2, (j - 1) % 2
+        wb = pb if pend[0] else b  # the row buffer this frame's kernel writes (the fold, or its own rows)
+        if freed[wb] is not None:
+            stream.wait_event(freed[wb])
+        img = None
+        if n_rows:
+            renderer.render_rows_async(cam.cam, outs[b].data_ptr(), row0=row0, row_step=step,
+                                       n_rows=n_rows, output=args.output, d_stats_ptr=stats_ptr,
+                                       stream_ptr=stream.cuda_stream, out_stream_ptr=coll.cuda_stream,
+                                       deferred=True)
+        else:
+            rendered[b].record(stream)
+            coll.wait_event(rendered[b])
+        if pend[0]:
+            img = gather(outs[pb])
+            freed[pb] = torch.cuda.Event()
+            freed[pb].record(coll)
+        pend[0] = bool(n_rows) and renderer.fold_pending()
+        if not pend[0]:
+            img = gather(outs[b])
+            freed[b] = torch.cuda.Event()
+            freed[b].record(coll)
+        return img
+
+    def finish():
+        """The deferred loop's last frame: run its pending pass and gather it."""
+        if not pend[0]:
+            return None
+        renderer.flush()
+        pend[0] = False
+        b = (nframe[0] - 1) % 2
+        img = gather(outs[b])
+        freed[b] = torch.cuda.Event()
+        freed[b].record(coll)
+        return img
+
     def frame(stats_ptr=None):
+        if stream is not coll and args.pipeline == "deferred":
+            return frame_deferred(stats_ptr)
         b = nframe[0] % 2
         nframe[0] += 1
         buf = outs[b]
@@ -290,6 +341,7 @@ def run(args):
     for w in range(args.warmup):
         t_w = time.perf_counter()
         frame()
+        finish()
         torch.cuda.synchronize()
         if w == 0:
             first_ms = (time.perf_counter() - t_w) * 1e3
@@ -314,7 +366,10 @@ def run(args):
     t0 = time.perf_counter()
     img = None
     for k in range(args.steps):
-        img = frame(stats.data_ptr())
+        got = frame(stats.data_ptr())
+        img = got if got is not None else img
+    last = finish()  # the deferred loop's last frame (inside the timed region)
+    img = last if last is not None else img
     torch.cuda.synchronize()
     if grouped:
         dist.barrier()
@@ -372,11 +427,13 @@ def run(args):
     if world == 1 and not args.no_fast and n_rows:
         renderer.set_precision("f32")
         frame()
+        finish()
         torch.cuda.synchronize()
         renderer.enable_timing(True)
         tf0 = time.perf_counter()
         for _ in range(2):
             frame()
+        finish()
         torch.cuda.synchronize()
         tf = (time.perf_counter() - tf0) / 2
         fast = {"value": round(W * H * spp / tf / 1e6, 3), "unit": "Msamples/s", "dtype": "f32",

@@ -158,13 +158,32 @@ int rt_render_rows_async(rt_context* ctx, const rt_camera* cam, uint32_t output_
  * The context then alternates two per-sample buffers, so the next call's sample kernel on `stream`
  * does not wait for this call's reduce pass — the pass (HBM-bound, ≈0.25 ms at rank 0 of 8 on
  * config 4) overlaps the next sample kernel.  The output, and `d_stats`, are complete when
- * `out_stream` reaches the point of the call.  out_stream == NULL or == stream: rt_render_rows_async.
+ * `out_stream` reaches the point of the call.  Either stream may be NULL (the HIP null stream);
+ * out_stream == stream: rt_render_rows_async.
  * Workspace: twice direct mode's per-sample buffer. */
 int rt_render_rows_async_split(rt_context* ctx, const rt_camera* cam, uint32_t output_format,
                                uint32_t row0, uint32_t row_step, uint32_t n_rows,
                                void* d_out, void* d_stats, void* stream, void* out_stream);
-/* Waits for the context's last render and reports a failure the kernel recorded (RT_ERR_HIP: a
- * wave gave up waiting for a running-sum hand-off — a bug guard, never expected). */
+/* Deferred variant for frame pipelines (bench.py's N > 1 loop): like the split call, but a
+ * direct-mode call's reduce pass is left PENDING — the next deferred call's sample kernel folds it
+ * with the waves that run out of items while a few long paths finish (the launch's tail, where the
+ * CUs otherwise idle), and a short follow-up pass on that call's out_stream takes the chunks they left.
+ * So the output of call k is complete on ITS out_stream once call k+1 has been issued and its
+ * out_stream reaches that point, or after rt_context_flush(ctx) / rt_context_sync(ctx), which run a
+ * pending pass whole.  A call that cannot fold the pending pass (a plain or ring-mode call, another
+ * launch size) runs it first.  Ring-mode calls behave as rt_render_rows_async_split.  out_stream
+ * (NULL: the HIP null stream) must differ from stream.  A caller that destroys the context with a pass pending gets no output
+ * for that call. */
+int rt_render_rows_async_deferred(rt_context* ctx, const rt_camera* cam, uint32_t output_format,
+                                  uint32_t row0, uint32_t row_step, uint32_t n_rows,
+                                  void* d_out, void* d_stats, void* stream, void* out_stream);
+/* Runs a pending deferred reduce pass (on the out_stream of the call that deferred it); no-op otherwise. */
+int rt_context_flush(rt_context* ctx);
+/* *pending = 1 if the last deferred call left its output pending (direct mode), else 0. */
+int rt_context_fold_pending(rt_context* ctx, int* pending);
+/* Waits for the context's last render (running a pending deferred reduce pass first) and reports a
+ * failure the kernel recorded (RT_ERR_HIP: a wave gave up waiting for a running-sum hand-off — a bug
+ * guard, never expected). */
 int rt_context_sync(rt_context* ctx);
 /* Arithmetic of the context's later renders: rt_precision (default RT_PRECISION_F64).  F32 needs
  * the BVH walk (any scene whose BVH builds); otherwise the parity kernel runs. */

@@ -69,6 +69,18 @@ constexpr uint32_t kStallBaseSec = 40;          // default bound; list walks sca
 constexpr uint32_t kStallMaxSec = 10000;        // < 2^32 units
 constexpr uint64_t kDirectBytes = 2ull << 30;  // direct mode when P x spp x 24 B fits
 
+// Deferred reduce pass (rt_render_rows_async_deferred): the previous direct-mode call's stored
+// samples, folded by this launch's waves once the item queue has run dry (the launch's tail, where
+// CUs otherwise idle behind a few long paths); chunks of 64 pixels claimed from `ctr` (zeroed before
+// the launch); a follow-up pass (fold_rest_kernel) takes the chunks left unclaimed.
+struct FoldArgs {
+    const double* samples;     // [spp][P][3]; nullptr: nothing to fold
+    void* out;                 // [P][3] f64 linear or u8 RGB
+    unsigned long long* ctr;   // chunk claim counter
+    uint32_t P, spp, format, n_chunks;
+    double scale;
+};
+
 struct UnitArgs {
     double* ring;              // [waves][kSlots][kUnitS * 64][3] wave-private sample colors
     double* sums;              // [P][3] running per-pixel sums (write-through hand-off between waves)
@@ -85,6 +97,7 @@ struct UnitArgs {
     uint32_t ring_waves;       // ring capacity in waves (the launch never has more)
     uint32_t stall_ticks;      // bound on one continuous hand-off wait, wait_clock units (2.56 µs, rt_units.h)
     double scale;              // pixelSamplesScale
+    FoldArgs fold;             // direct mode: a previous call's samples to fold in the tail (may be empty)
 };
 
 // samples [*s0, *s0 + *n) of chunk k (the table is read-only: scalar loads)
@@ -213,6 +226,7 @@ __host__ __device__ inline uint32_t bvh_leaves_offset(uint32_t n_nodes) {
 // small launch), before the ring's bound — the runtime sizes the ring to it (ua may be null then).
 // Direct mode's second pass: per pixel, the stored colors added in sample order, scaled, written.
 extern "C" hipError_t rtk_launch_reduce(const rtk::UnitArgs* ua, hipStream_t stream);
+extern "C" hipError_t rtk_launch_fold_rest(const rtk::FoldArgs* f, hipStream_t stream);
 extern "C" hipError_t rtk_launch_samples(const rtk::KernelParams* p, const rtk::GeoRec* geo,
                                          const rtk::MatRec* mat, const rtk::UnitArgs* ua,
                                          void* stats, hipStream_t stream, const char** name, bool direct,

@@ -1154,6 +1154,46 @@ __device__ __forceinline__ void shade_f32(int k, float t, const GeoRec* __restri
     }
 }
 
+// Direct mode's reduce pass for one pixel (reduce_kernel, and the deferred fold below).
+__device__ __forceinline__ void reduce_pixel(const double* __restrict__ samples, uint32_t P, uint32_t spp, uint32_t q,
+                                             void* out, uint32_t format, double scale) {
+    const double* src = samples + 3 * (size_t)q;
+    const size_t stride = 3 * (size_t)P;
+    double x = 0.0, y = 0.0, z = 0.0;
+#pragma unroll 8
+    for (uint32_t s = 0; s < spp; ++s) {
+        x = x + src[0];
+        y = y + src[1];
+        z = z + src[2];
+        src += stride;
+    }
+    if (format == 0) {
+        double* o = (double*)out + 3 * (size_t)q;
+        o[0] = x * scale;
+        o[1] = y * scale;
+        o[2] = z * scale;
+    } else {
+        uint8_t* o = (uint8_t*)out + 3 * (size_t)q;
+        o[0] = to_byte(x * scale);
+        o[1] = to_byte(y * scale);
+        o[2] = to_byte(z * scale);
+    }
+}
+
+// The deferred reduce pass: a wave claims chunks of 64 pixels until none is left (the same sums as
+// reduce_kernel, lane l one pixel).  Run by the drained waves of the next direct-mode launch and by
+// fold_rest_kernel for what they left.
+__device__ __forceinline__ void fold_chunks(const FoldArgs& f, uint32_t lane) {
+    while (true) {
+        uint32_t c = 0;
+        if (lane == 0) c = (uint32_t)atomicAdd(f.ctr, 1ull);
+        c = __builtin_amdgcn_readfirstlane(__shfl(c, 0, 64));
+        if (c >= f.n_chunks) break;
+        const uint32_t q = c * 64 + lane;
+        if (q < f.P) reduce_pixel(f.samples, f.P, f.spp, q, f.out, f.format, f.scale);
+    }
+}
+
 // ------------------------------------------------------------------------------------------------
 // The path state machine shared by every kernel variant: unit refill (rt_units.h) + one ray segment
 // per lane per iteration (rayColor's loop body, camera.zig:153-177) + ring stores of finished
@@ -1481,6 +1521,11 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
         }
     }
 
+    // the previous direct-mode call's reduce pass, taken up by the waves that ran out of items while a
+    // few long paths finish elsewhere (rt_render_rows_async_deferred; empty otherwise)
+    if constexpr (kDirect && !kProf) {
+        if (ua.fold.samples != nullptr) fold_chunks(ua.fold, lane);
+    }
     RTK_MARK("epilogue");
     if (stats) {
         // wave-level reduction, one atomic pair per wave (all lanes converged here)
@@ -1641,28 +1686,10 @@ template <int kOut>
 __global__ __launch_bounds__(256) void reduce_kernel(UnitArgs ua) {
     const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
     if (q >= ua.P) return;
-    const double* src = ua.samples + 3 * (size_t)q;
-    const size_t stride = 3 * (size_t)ua.P;
-    double x = 0.0, y = 0.0, z = 0.0;
-#pragma unroll 8
-    for (uint32_t s = 0; s < ua.spp; ++s) {
-        x = x + src[0];
-        y = y + src[1];
-        z = z + src[2];
-        src += stride;
-    }
-    if constexpr (kOut == 0) {
-        double* o = (double*)ua.out + 3 * (size_t)q;
-        o[0] = x * ua.scale;
-        o[1] = y * ua.scale;
-        o[2] = z * ua.scale;
-    } else {
-        uint8_t* o = (uint8_t*)ua.out + 3 * (size_t)q;
-        o[0] = to_byte(x * ua.scale);
-        o[1] = to_byte(y * ua.scale);
-        o[2] = to_byte(z * ua.scale);
-    }
+    reduce_pixel(ua.samples, ua.P, ua.spp, q, ua.out, kOut, ua.scale);
 }
+
+__global__ __launch_bounds__(256) void fold_rest_kernel(FoldArgs f) { fold_chunks(f, lane_id()); }
 
 }  // namespace rtk
 
@@ -1857,6 +1884,14 @@ extern "C" hipError_t rtk_launch_samples_fast(const rtk::KernelParams* p, const 
                                               hipStream_t stream, const char** name, bool direct,
                                               uint32_t* plan_waves) {
     return launch_bvh<true>(p, b, geo, mat, ua, stats, stream, name, direct, plan_waves);
+}
+
+extern "C" hipError_t rtk_launch_fold_rest(const rtk::FoldArgs* f, hipStream_t stream) {
+    using namespace rtk;
+    if (f->samples == nullptr || f->n_chunks == 0) return hipErrorInvalidValue;
+    const uint32_t blocks = (f->n_chunks + 3) / 4;  // at most one wave per chunk; the rest exit at once
+    hipLaunchKernelGGL(fold_rest_kernel, dim3(blocks), dim3(256), 0, stream, *f);
+    return hipGetLastError();
 }
 
 extern "C" hipError_t rtk_launch_reduce(const rtk::UnitArgs* ua, hipStream_t stream) {

@@ -101,6 +101,14 @@ struct rt_context {
     uint32_t samples_flip = 0;      // the buffer the next split call's samples go to
     hipEvent_t reduced[2] = {nullptr, nullptr};  // the last reduce pass that read buffer 0 / 1 has ended
     bool reduced_valid[2] = {false, false};
+    // a deferred call's reduce pass not yet run (rt_render_rows_async_deferred): its samples sit in
+    // buffer fold_buf, its output is promised on fold_stream; the next deferred call's drained waves
+    // fold it, or flush_fold runs it whole
+    bool fold_pending = false;
+    uint32_t fold_buf = 0;
+    rtk::FoldArgs fold{};
+    hipStream_t fold_stream = nullptr;
+    unsigned long long* d_fold_ctr = nullptr;  // 2 chunk counters, 128 B apart
     std::vector<uint32_t> sched;    // chunk table of the last launch (rt_schedule.hpp), and its copy
     uint32_t* d_sched = nullptr;
     size_t sched_bytes = 0;
@@ -387,8 +395,27 @@ bool same_spheres(const SceneData& sd, const rt_sphere* s, size_t n) {
     return sd.spheres.size() == n && n && std::memcmp(sd.spheres.data(), s, n * sizeof(rt_sphere)) == 0;
 }
 
-// Waits until the device has finished the context's last render (before rewriting its buffers).
+// Runs a deferred call's pending reduce pass whole, on the stream its output was promised on, after
+// the last launch (which wrote or folded nothing of it since it is still pending).
+int flush_fold(rt_context* ctx) {
+    if (!ctx->fold_pending) return RT_OK;
+    ctx->fold_pending = false;
+    hipStream_t fs = ctx->fold_stream;
+    if (ctx->launched_valid) HIP_CHECK(hipStreamWaitEvent(fs, ctx->launched, 0));
+    HIP_CHECK(hipMemsetAsync(ctx->fold.ctr, 0, sizeof(unsigned long long), fs));
+    HIP_CHECK(rtk_launch_fold_rest(&ctx->fold, fs));
+    HIP_CHECK(hipEventRecord(ctx->reduced[ctx->fold_buf], fs));
+    ctx->reduced_valid[ctx->fold_buf] = true;
+    HIP_CHECK(hipEventRecord(ctx->done, fs));
+    ctx->done_valid = true;
+    return RT_OK;
+}
+
+// Waits until the device has finished the context's last render (before rewriting its buffers); a
+// pending deferred reduce pass is run first.
 int quiesce(rt_context* ctx) {
+    int rc = flush_fold(ctx);
+    if (rc) return rc;
     if (ctx->done_valid) HIP_CHECK(hipEventSynchronize(ctx->done));
     HIP_CHECK(hipStreamSynchronize(ctx->stream));
     return RT_OK;
@@ -658,7 +685,7 @@ int rt_context_destroy(rt_context* ctx) {
     if (ctx->done_valid) (void)hipEventSynchronize(ctx->done);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     for (void* p : {(void*)ctx->d_geo, (void*)ctx->d_mat, (void*)ctx->d_ring, (void*)ctx->d_sums, (void*)ctx->d_flags,
-                    (void*)ctx->d_samples, (void*)ctx->d_samples2, (void*)ctx->d_sched, (void*)ctx->d_ctr, (void*)ctx->d_nodes, (void*)ctx->d_leaves, (void*)ctx->d_always_geo,
+                    (void*)ctx->d_samples, (void*)ctx->d_samples2, (void*)ctx->d_fold_ctr, (void*)ctx->d_sched, (void*)ctx->d_ctr, (void*)ctx->d_nodes, (void*)ctx->d_leaves, (void*)ctx->d_always_geo,
                     (void*)ctx->d_always_sid, ctx->d_out, (void*)ctx->d_stats})
         (void)hipFree(p);
     if (ctx->h_out) (void)hipHostFree(ctx->h_out);
@@ -705,12 +732,13 @@ int rt_context_sync(rt_context* ctx) {
 
 namespace {
 
-// One render call.  os == nullptr: everything on s (rt_render_rows_async).  Otherwise the output is
-// completed in os's order: direct mode's reduce pass runs on os after the sample kernel on s, over
+// One render call.  !split: everything on s (rt_render_rows_async).  Otherwise the output is
+// completed in os's order (os may be the null stream): direct mode's reduce pass runs on os after the sample kernel on s, over
 // one of two per-sample buffers taken in turn, so the next call's sample kernel on s need not wait
 // for this call's reduce pass (rt_render_rows_async_split).
 int render_rows(rt_context* ctx, const rt_camera* cam, uint32_t output_format, uint32_t row0, uint32_t row_step,
-                uint32_t n_rows, void* d_out, void* d_stats, hipStream_t s, hipStream_t os) {
+                uint32_t n_rows, void* d_out, void* d_stats, hipStream_t s, hipStream_t os, bool split,
+                bool defer) {
     if (!ctx) { rt_set_last_error("null context"); return RT_ERR_INVALID; }
     int rc = validate_camera(cam);
     if (rc) return rc;
@@ -725,7 +753,7 @@ int render_rows(rt_context* ctx, const rt_camera* cam, uint32_t output_format, u
         return RT_ERR_INVALID;
     }
     HIP_CHECK(hipSetDevice(ctx->device));
-    if (os == s) os = nullptr;  // one stream: the plain call
+    if (os == s) split = defer = false;  // one stream: the plain call (os may be the null stream)
 
     // camera-ray origins (center + defocus disk) must lie inside the BVH padding's origin bound
     // (lanes outside it would walk without culling: correct, but every camera ray would pay)
@@ -791,9 +819,18 @@ int render_rows(rt_context* ctx, const rt_camera* cam, uint32_t output_format, u
                                           direct, plan_waves);
         return rtk_launch_samples(&p, ctx->d_geo, ctx->d_mat, u, d_stats, s, &ctx->last_kernel, direct, plan_waves);
     };
+    // deferred calls (direct mode, an output stream): this call's reduce pass is left pending for the
+    // next deferred call's drained waves; a pending pass this call will not fold (a plain or ring-mode
+    // call, another launch size) runs whole first
+    const bool defer_fold = defer && direct && split;
+    if (ctx->fold_pending && !(defer_fold && ctx->fold.P == (uint32_t)P && ctx->fold.spp == cam->samples_per_pixel &&
+                               ctx->fold_buf == (ctx->samples_flip ^ 1u))) {
+        rc = flush_fold(ctx);
+        if (rc) return rc;
+    }
     // a context holds the workspace of one mode at a time (rt.h "Workspace"); split calls in direct
     // mode alternate two per-sample buffers
-    const bool split_reduce = direct && os != nullptr;
+    const bool split_reduce = direct && split;
     uint32_t sbuf = 0;
     if (direct) {
         rc = release_buffer(ctx, (void**)&ctx->d_ring, &ctx->ring_bytes);
@@ -823,6 +860,10 @@ int render_rows(rt_context* ctx, const rt_camera* cam, uint32_t output_format, u
     }
     const size_t flag_bytes = (n_tiles * sizeof(uint32_t) + 15) & ~(size_t)15;  // memset in 16-B multiples
     if (!rc) rc = ensure_buffer(ctx, (void**)&ctx->d_flags, &ctx->flags_bytes, flag_bytes);
+    if (!rc && defer_fold && !ctx->d_fold_ctr) {
+        size_t fb = 0;
+        rc = ensure_buffer(ctx, (void**)&ctx->d_fold_ctr, &fb, 2 * 16 * sizeof(unsigned long long));
+    }
     if (!rc && !ctx->d_ctr) {
         size_t cb = 0;
         rc = ensure_buffer(ctx, (void**)&ctx->d_ctr, &cb, rtk::kCtrBytes);
@@ -871,6 +912,12 @@ int render_rows(rt_context* ctx, const rt_camera* cam, uint32_t output_format, u
     // writes may still be read by the reduce pass of an earlier call (on any stream)
     if (ctx->launched_valid && ctx->launched_stream != s) HIP_CHECK(hipStreamWaitEvent(s, ctx->launched, 0));
     if (direct && ctx->reduced_valid[sbuf]) HIP_CHECK(hipStreamWaitEvent(s, ctx->reduced[sbuf], 0));
+    // the pending pass this launch folds in its tail (the flush above left only a foldable one)
+    const bool folding = defer_fold && ctx->fold_pending;
+    if (folding) {
+        ua.fold = ctx->fold;
+        HIP_CHECK(hipMemsetAsync(ctx->fold.ctr, 0, sizeof(unsigned long long), s));
+    }
     HIP_CHECK(hipMemsetAsync(ctx->d_ctr, 0, rtk::kCtrLaunchBytes, s));  // not the sticky error word
     if (!direct) HIP_CHECK(hipMemsetAsync(ctx->d_flags, 0, flag_bytes, s));
     hipEvent_t* ev = ctx->timing ? &ctx->events[kEventsPerCall * ctx->call_first] : nullptr;
@@ -882,12 +929,33 @@ int render_rows(rt_context* ctx, const rt_camera* cam, uint32_t output_format, u
     ctx->launched_stream = s;
     // the stream on which the output is complete: split calls continue on os, after the sample kernel
     hipStream_t rs = s;
-    if (os) {
+    if (split) {
         HIP_CHECK(hipStreamWaitEvent(os, ctx->launched, 0));
         rs = os;
     }
     if (ev) HIP_CHECK(hipEventRecord(ev[2], rs));
-    if (direct) {
+    if (folding) {
+        // the chunks of the previous deferred call that no drained wave took
+        HIP_CHECK(rtk_launch_fold_rest(&ctx->fold, rs));
+        HIP_CHECK(hipEventRecord(ctx->reduced[ctx->fold_buf], rs));
+        ctx->reduced_valid[ctx->fold_buf] = true;
+        ctx->fold_pending = false;
+    }
+    if (defer_fold) {
+        rtk::FoldArgs f{};
+        f.samples = ua.samples;
+        f.out = d_out;
+        f.ctr = ctx->d_fold_ctr + 16 * sbuf;
+        f.P = (uint32_t)P;
+        f.spp = cam->samples_per_pixel;
+        f.format = output_format;
+        f.n_chunks = (uint32_t)((P + 63) / 64);
+        f.scale = ua.scale;
+        ctx->fold = f;
+        ctx->fold_buf = sbuf;
+        ctx->fold_stream = rs;
+        ctx->fold_pending = true;
+    } else if (direct) {
         HIP_CHECK(rtk_launch_reduce(&ua, rs));
         HIP_CHECK(hipEventRecord(ctx->reduced[sbuf], rs));
         ctx->reduced_valid[sbuf] = true;
@@ -905,14 +973,38 @@ extern "C" {
 int rt_render_rows_async(rt_context* ctx, const rt_camera* cam, uint32_t output_format, uint32_t row0,
                          uint32_t row_step, uint32_t n_rows, void* d_out, void* d_stats, void* stream) {
     // NULL = the HIP null stream, like torch's default stream
-    return render_rows(ctx, cam, output_format, row0, row_step, n_rows, d_out, d_stats, (hipStream_t)stream, nullptr);
+    return render_rows(ctx, cam, output_format, row0, row_step, n_rows, d_out, d_stats, (hipStream_t)stream, nullptr,
+                       false, false);
 }
 
 int rt_render_rows_async_split(rt_context* ctx, const rt_camera* cam, uint32_t output_format, uint32_t row0,
                                uint32_t row_step, uint32_t n_rows, void* d_out, void* d_stats, void* stream,
                                void* out_stream) {
     return render_rows(ctx, cam, output_format, row0, row_step, n_rows, d_out, d_stats, (hipStream_t)stream,
-                       (hipStream_t)out_stream);
+                       (hipStream_t)out_stream, true, false);
+}
+
+int rt_render_rows_async_deferred(rt_context* ctx, const rt_camera* cam, uint32_t output_format, uint32_t row0,
+                                  uint32_t row_step, uint32_t n_rows, void* d_out, void* d_stats, void* stream,
+                                  void* out_stream) {
+    if (out_stream == stream) {
+        rt_set_last_error("rt_render_rows_async_deferred needs an out_stream other than stream");
+        return RT_ERR_INVALID;
+    }
+    return render_rows(ctx, cam, output_format, row0, row_step, n_rows, d_out, d_stats, (hipStream_t)stream,
+                       (hipStream_t)out_stream, true, true);
+}
+
+int rt_context_fold_pending(rt_context* ctx, int* pending) {
+    if (!ctx || !pending) { rt_set_last_error("null context / output"); return RT_ERR_INVALID; }
+    *pending = ctx->fold_pending ? 1 : 0;
+    return RT_OK;
+}
+
+int rt_context_flush(rt_context* ctx) {
+    if (!ctx) { rt_set_last_error("null context"); return RT_ERR_INVALID; }
+    HIP_CHECK(hipSetDevice(ctx->device));
+    return flush_fold(ctx);
 }
 
 int rt_context_enable_timing(rt_context* ctx, int enable) {
@@ -977,7 +1069,7 @@ const char* rt_kernel_name(rt_context* ctx) { return ctx ? ctx->last_kernel : "r
 int rt_context_workspace_bytes(rt_context* ctx, uint64_t* bytes) {
     if (!ctx || !bytes) { rt_set_last_error("null context / output"); return RT_ERR_INVALID; }
     *bytes = (uint64_t)ctx->ring_bytes + ctx->sums_bytes + ctx->flags_bytes + ctx->samples_bytes + ctx->samples2_bytes +
-             ctx->sched_bytes +
+             ctx->sched_bytes + (ctx->d_fold_ctr ? 2 * 16 * sizeof(unsigned long long) : 0) +
              (ctx->d_ctr ? rtk::kCtrBytes : 0);
     return RT_OK;
 }

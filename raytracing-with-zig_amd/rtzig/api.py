@@ -192,23 +192,41 @@ class DeviceRenderer:
         check("rt_context_set_scene", self.lib.rt_context_set_scene(self.ctx, spheres, n))
 
     def render_rows_async(self, cam, d_out_ptr, row0=0, row_step=1, n_rows=None, output="linear",
-                          d_stats_ptr=None, stream_ptr=None, out_stream_ptr=None):
+                          d_stats_ptr=None, stream_ptr=None, out_stream_ptr=None, deferred=False):
         """out_stream_ptr: complete the output on that stream instead (rt_render_rows_async_split:
         direct mode's reduce pass runs there, over two per-sample buffers taken in turn, so it
-        overlaps the next call's sample kernel on stream_ptr)."""
+        overlaps the next call's sample kernel on stream_ptr).  deferred (with out_stream_ptr):
+        rt_render_rows_async_deferred — this call's output completes after the NEXT deferred call (or
+        flush() / sync()), its reduce pass folded by that call's drained waves."""
         if n_rows is None:
             n_rows = (cam.image_height - row0 + row_step - 1) // row_step
         fmt = abi.RT_OUT_LINEAR_F64 if output == "linear" else abi.RT_OUT_RGB8
-        if out_stream_ptr:
+        if deferred:  # out_stream_ptr 0 is the HIP null stream (torch's default stream)
+            check("rt_render_rows_async_deferred",
+                  self.lib.rt_render_rows_async_deferred(self.ctx, C.byref(cam), fmt, row0, row_step, n_rows,
+                                                         C.c_void_p(d_out_ptr), C.c_void_p(d_stats_ptr or 0),
+                                                         C.c_void_p(stream_ptr or 0), C.c_void_p(out_stream_ptr or 0)))
+            return
+        if out_stream_ptr is not None:
             check("rt_render_rows_async_split",
                   self.lib.rt_render_rows_async_split(self.ctx, C.byref(cam), fmt, row0, row_step, n_rows,
                                                       C.c_void_p(d_out_ptr), C.c_void_p(d_stats_ptr or 0),
-                                                      C.c_void_p(stream_ptr or 0), C.c_void_p(out_stream_ptr)))
+                                                      C.c_void_p(stream_ptr or 0), C.c_void_p(out_stream_ptr or 0)))
             return
         check("rt_render_rows_async",
               self.lib.rt_render_rows_async(self.ctx, C.byref(cam), fmt, row0, row_step, n_rows,
                                             C.c_void_p(d_out_ptr), C.c_void_p(d_stats_ptr or 0),
                                             C.c_void_p(stream_ptr or 0)))
+
+    def flush(self):
+        """Runs a pending deferred reduce pass (rt_context_flush)."""
+        check("rt_context_flush", self.lib.rt_context_flush(self.ctx))
+
+    def fold_pending(self):
+        """True if the last deferred call left its output pending (its reduce pass not yet run)."""
+        v = C.c_int()
+        check("rt_context_fold_pending", self.lib.rt_context_fold_pending(self.ctx, C.byref(v)))
+        return bool(v.value)
 
     def sync(self):
         """Waits for the last render; raises if the kernel recorded a failure."""

@@ -19,6 +19,9 @@ EXPORTED = [
     "rt_context_set_scene",
     "rt_render_rows_async",
     "rt_render_rows_async_split",
+    "rt_render_rows_async_deferred",
+    "rt_context_flush",
+    "rt_context_fold_pending",
     "rt_kernel_name",
     "rt_context_workspace_bytes",
     "rt_context_enable_timing",
@@ -65,6 +68,10 @@ def _declare(lib):
                                            C.c_uint32, vp, vp, vp]),
         "rt_render_rows_async_split": (C.c_int, [vp, P(RtCamera), C.c_uint32, C.c_uint32, C.c_uint32,
                                                  C.c_uint32, vp, vp, vp, vp]),
+        "rt_render_rows_async_deferred": (C.c_int, [vp, P(RtCamera), C.c_uint32, C.c_uint32, C.c_uint32,
+                                                    C.c_uint32, vp, vp, vp, vp]),
+        "rt_context_flush": (C.c_int, [vp]),
+        "rt_context_fold_pending": (C.c_int, [vp, P(C.c_int)]),
         "rt_kernel_name": (C.c_char_p, [vp]),
         "rt_context_workspace_bytes": (C.c_int, [vp, P(C.c_uint64)]),
         "rt_context_enable_timing": (C.c_int, [vp, C.c_int]),

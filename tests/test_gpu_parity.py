@@ -675,3 +675,94 @@ def test_split_render_pipeline_bit_exact(oracle, mode, monkeypatch):
         assert np.array_equal(img.cpu().numpy(), ref)
     st = stats.cpu().tolist()
     assert st[1] == 4 * 12 * 1200 * 24 and st[0] == 4 * rays
+
+
+@pytest.mark.parametrize("mode", ["direct", "ring"])
+def test_deferred_render_pipeline_bit_exact(oracle, mode, monkeypatch):
+    """rt_render_rows_async_deferred: a direct-mode call's reduce pass is left pending and folded by
+    the next deferred call's drained waves (plus a follow-up pass for the chunks they left); the last
+    one by rt_context_flush.  Five frames into two row buffers, each taken on the second stream once
+    it is complete (after the next call, or after the flush), interleaved with a plain call that must
+    run the pending pass first: every frame bit-exact against oracle B, exact sample counts (reference:
+    the row loop camera.zig:128-138 that a rank's launch replaces)."""
+    import torch
+    monkeypatch.setenv("RTZIG_UNIT_MODE", mode)
+    cam = rtzig.final_scene_camera(width=1200, aspect_ratio=1.5, spp=24)
+    ref, rays = oracle.render_b(cam.cam, cam.scene.world, row0=5, row_step=8, n_rows=12, threads=16)
+    r = rtzig.DeviceRenderer(0)
+    r.set_scene(cam.scene.world)
+    render, coll = torch.cuda.Stream(), torch.cuda.Stream()
+    outs = [torch.zeros((12, 1200, 3), dtype=torch.float64, device="cuda:0") for _ in range(2)]
+    stats = torch.zeros(2, dtype=torch.int64, device="cuda:0")
+    got = []
+    pending = False
+    for k in range(5):
+        render.wait_stream(coll)  # the copies below have read the buffer this call may write
+        r.render_rows_async(cam.cam, outs[k % 2].data_ptr(), row0=5, row_step=8, n_rows=12,
+                            d_stats_ptr=stats.data_ptr(), stream_ptr=render.cuda_stream,
+                            out_stream_ptr=coll.cuda_stream, deferred=True)
+        with torch.cuda.stream(coll):
+            if pending:
+                got.append(outs[(k - 1) % 2].clone())  # frame k-1, completed by this call
+        pending = r.fold_pending()
+        assert pending == (mode == "direct")
+        if not pending:
+            with torch.cuda.stream(coll):
+                got.append(outs[k % 2].clone())
+        if k == 2:
+            # a plain call in between runs the pending pass whole first
+            plain = torch.zeros_like(outs[0])
+            r.render_rows_async(cam.cam, plain.data_ptr(), row0=5, row_step=8, n_rows=12, stream_ptr=render.cuda_stream)
+            assert not r.fold_pending()
+            with torch.cuda.stream(coll):
+                if pending:
+                    got.append(outs[k % 2].clone())
+            pending = False
+            torch.cuda.synchronize()
+            assert np.array_equal(plain.cpu().numpy(), ref)
+    r.flush()
+    with torch.cuda.stream(coll):
+        if pending:
+            got.append(outs[4 % 2].clone())
+    torch.cuda.synchronize()
+    r.sync()
+    r.close()
+    assert len(got) == 5
+    for img in got:
+        assert np.array_equal(img.cpu().numpy(), ref)
+    st = stats.cpu().tolist()
+    assert st[1] == 5 * 12 * 1200 * 24 and st[0] == 5 * rays
+
+
+def test_split_and_deferred_on_the_null_stream(oracle, monkeypatch):
+    """The output stream may be the HIP null stream (torch's default stream, handle 0 — the
+    collective stream of bench.py): split and deferred calls then complete the output there, ordered
+    after the sample kernel on the render stream.  Direct-mode rows, three frames each way, every
+    frame bit-exact against oracle B."""
+    import torch
+    monkeypatch.setenv("RTZIG_UNIT_MODE", "direct")
+    cam = rtzig.final_scene_camera(width=1200, aspect_ratio=1.5, spp=24)
+    ref, _ = oracle.render_b(cam.cam, cam.scene.world, row0=2, row_step=8, n_rows=12, threads=16)
+    r = rtzig.DeviceRenderer(0)
+    r.set_scene(cam.scene.world)
+    render, null = torch.cuda.Stream(), torch.cuda.default_stream()
+    assert null.cuda_stream == 0
+    outs = [torch.zeros((12, 1200, 3), dtype=torch.float64, device="cuda:0") for _ in range(3)]
+    for k in range(3):  # split
+        r.render_rows_async(cam.cam, outs[k].data_ptr(), row0=2, row_step=8, n_rows=12,
+                            stream_ptr=render.cuda_stream, out_stream_ptr=0)
+    null.synchronize()  # the null stream alone: its order must cover the outputs
+    got = [o.clone() for o in outs]
+    torch.cuda.synchronize()
+    outs = [torch.zeros_like(outs[0]) for _ in range(3)]
+    for k in range(3):  # deferred
+        r.render_rows_async(cam.cam, outs[k].data_ptr(), row0=2, row_step=8, n_rows=12,
+                            stream_ptr=render.cuda_stream, out_stream_ptr=0, deferred=True)
+    r.flush()
+    null.synchronize()
+    got += [o.clone() for o in outs]
+    torch.cuda.synchronize()
+    r.sync()
+    r.close()
+    for img in got:
+        assert np.array_equal(img.cpu().numpy(), ref)

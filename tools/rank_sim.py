@@ -43,6 +43,8 @@ ap.add_argument("--pipe-frames", type=int, default=0,
                 help="also time each rank's rows in bench.py's frame pipeline (two row buffers, render "
                      "stream, output completed on a second stream: rt_render_rows_async_split), this many "
                      "frames, wall clock per frame")
+ap.add_argument("--pipe-mode", choices=["split", "deferred"], default="deferred",
+                help="the pipeline's render call (bench.py --pipeline)")
 args = ap.parse_args()
 
 cam = rtzig.final_scene_camera(width=args.width, aspect_ratio=args.aspect, spp=args.spp)
@@ -64,29 +66,46 @@ def kernel_ms(row0, step, n_rows):
 
 def pipeline_ms(row0, step, n_rows):
     """bench.py's N > 1 loop without the collective: frame k renders into buffer k % 2 on the render
-    stream with its output (direct mode: the reduce pass) completed on the second stream, where the
-    gather would run; wall clock per frame over args.pipe_frames frames."""
+    stream with its output completed on the second stream, where the gather would run (split: the
+    reduce pass there; deferred: folded by the next frame's drained waves, the last one flushed);
+    wall clock per frame over args.pipe_frames frames."""
     render, coll = torch.cuda.Stream(), torch.cuda.Stream()
     outs = [torch.empty((n_rows, W, 3), dtype=torch.float64, device="cuda:0") for _ in range(2)]
     freed = [None, None]
+    pend = [False]
+    deferred = args.pipe_mode == "deferred"
 
     def frame(k):
-        b = k % 2
-        if freed[b] is not None:
-            render.wait_event(freed[b])
+        b, pb = k % 2, (k - 1) % 2
+        wb = pb if pend[0] else b  # the row buffer this frame's kernel writes (deferred fold, or its own rows)
+        if freed[wb] is not None:
+            render.wait_event(freed[wb])
         r.render_rows_async(cam.cam, outs[b].data_ptr(), row0=row0, row_step=step, n_rows=n_rows,
-                            stream_ptr=render.cuda_stream, out_stream_ptr=coll.cuda_stream)
-        freed[b] = torch.cuda.Event()
-        freed[b].record(coll)
+                            stream_ptr=render.cuda_stream, out_stream_ptr=coll.cuda_stream, deferred=deferred)
+        if pend[0]:
+            freed[pb] = torch.cuda.Event()
+            freed[pb].record(coll)
+        pend[0] = deferred and r.fold_pending()
+        if not pend[0]:
+            freed[b] = torch.cuda.Event()
+            freed[b].record(coll)
+
+    def finish():
+        if pend[0]:
+            r.flush()
+            pend[0] = False
 
     for k in range(2):
         frame(k)
+    finish()
     torch.cuda.synchronize()
     best = None
     for _ in range(args.reps):
+        freed[0] = freed[1] = None
         t0 = time.perf_counter()
         for k in range(args.pipe_frames):
             frame(k)
+        finish()
         torch.cuda.synchronize()
         ms = (time.perf_counter() - t0) / args.pipe_frames * 1e3
         best = ms if best is None else min(best, ms)

@@ -46,8 +46,25 @@ def main():
         done = [torch.cuda.Event() for _ in range(2)]
         freed = [None, None]
 
+        pend = [False]
+
         def frame(k, split):
             b = k % 2
+            if split == "deferred":
+                # kernel k folds frame k-1 into buffer (k-1) % 2, last read by frame k-3's consumer
+                pb = (k - 1) % 2
+                if pend[0] and freed[pb] is not None:
+                    render.wait_event(freed[pb])
+                r.render_rows_async(cam.cam, outs[b].data_ptr(), row0=0, row_step=N, n_rows=rows,
+                                    stream_ptr=render.cuda_stream, out_stream_ptr=coll.cuda_stream, deferred=True)
+                if pend[0]:
+                    freed[pb] = torch.cuda.Event()
+                    freed[pb].record(coll)  # frame k-1's output is complete on coll here
+                pend[0] = r.fold_pending()
+                if not pend[0]:
+                    freed[b] = torch.cuda.Event()
+                    freed[b].record(coll)
+                return
             if freed[b] is not None:
                 render.wait_event(freed[b])
             if split:
@@ -61,18 +78,28 @@ def main():
             freed[b] = torch.cuda.Event()
             freed[b].record(coll)  # the consumer of this buffer (bench: dist.gather) has run
 
-        for split in (False, True):  # warm (tree, workspace of both modes)
+        modes = (False, True, "deferred")
+
+        def finish(split):
+            if split == "deferred":
+                r.flush()  # the last frame's pass, on coll
+                pend[0] = False
+                freed[0] = freed[1] = None
+
+        for split in modes:  # warm (tree, workspace of every mode)
             for k in range(2):
                 frame(k, split)
+            finish(split)
         torch.cuda.synchronize()
         ref = outs[0].clone()
-        res = {False: [], True: []}
+        res = {m: [] for m in modes}
         for rd in range(args.rounds):
-            for split in (False, True):
+            for split in modes:
                 torch.cuda.synchronize()
                 t0 = time.perf_counter()
                 for k in range(args.steps):
                     frame(k, split)
+                finish(split)
                 torch.cuda.synchronize()
                 ms = (time.perf_counter() - t0) / args.steps * 1e3
                 same = all(torch.equal(o, ref) for o in outs)
@@ -83,7 +110,8 @@ def main():
                     raise SystemExit("split_ab: outputs differ")
         med = {k: sorted(v)[len(v) // 2] for k, v in res.items()}
         summary[N] = {"rows": rows, "ms_plain": round(med[False], 4), "ms_split": round(med[True], 4),
-                      "speedup": round(med[False] / med[True], 4)}
+                      "ms_deferred": round(med["deferred"], 4), "speedup": round(med[False] / med[True], 4),
+                      "speedup_deferred": round(med[False] / med["deferred"], 4)}
     r.sync()
     r.close()
     print(json.dumps({"summary": summary, "steps": args.steps, "rounds": args.rounds, "spp": args.spp,
