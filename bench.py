@@ -145,7 +145,7 @@ def parse_args(argv=None):
                     help="at --gpus 1, still join a (1-rank) process group on --dist-backend and run the "
                          "N>1 pipeline: two row buffers, the render stream, and each frame's dist.gather on "
                          "the collective stream (nccl: the RCCL gather on one GPU)")
-    ap.add_argument("--pipeline", choices=["split", "deferred"], default="split",
+    ap.add_argument("--pipeline", choices=["split", "deferred"], default="deferred",
                     help="N > 1 frame loop: 'split' completes each frame's output on the collective stream "
                          "(rt_render_rows_async_split); 'deferred' also leaves a direct-mode frame's reduce "
                          "pass to the next frame's drained waves (rt_render_rows_async_deferred), gathering "
