@@ -497,8 +497,12 @@ def run(args):
                            + ((", RCCL gather to rank 0" if args.dist_backend == "nccl" else
                                ", gloo gather to rank 0 (rehearsal: ranks share devices)")
                               + (" (1-rank group, --collective)" if world == 1 else "")
-                              + ", each frame's gather (and a direct-mode reduce pass) overlapped with the next "
-                                "frame's render (two row buffers)"
+                              + (", each frame's gather overlapped with the next frame's render (two row buffers); "
+                                 "a direct-mode frame's reduce pass folded by the next frame's drained waves "
+                                 "(rt_render_rows_async_deferred)" if args.pipeline == "deferred" else
+                                 ", each frame's gather and a direct-mode reduce pass on the collective stream, "
+                                 "overlapped with the next frame's render (two row buffers; "
+                                 "rt_render_rows_async_split)")
                               if grouped else "")},
             "roofline": {
                 "bound": "valu",
