@@ -270,9 +270,12 @@ def run(args):
         j = nframe[0]
         nframe[0] += 1
         b, pb = j % 2, (j - 1) % 2
-        wb = pb if pend[0] else b  # the row buffer this frame's kernel writes (the fold, or its own rows)
-        if freed[wb] is not None:
-            stream.wait_event(freed[wb])
+        # the kernel writes its own rows into outs[b] (a call that cannot fold the pending pass runs it
+        # first and writes outs[b] directly), and with a pass pending it also folds into outs[pb]: both
+        # buffers' last gathers must have finished (in steady state both events have long completed)
+        for wb in ((b, pb) if pend[0] else (b,)):
+            if freed[wb] is not None:
+                stream.wait_event(freed[wb])
         img = None
         if n_rows:
             renderer.render_rows_async(cam.cam, outs[b].data_ptr(), row0=row0, row_step=step,
@@ -529,6 +532,11 @@ def run(args):
                 "kernel_ms_avg": round(k_frame_s * 1e3 / max(1.0, launches_per_frame), 3),
                 "unit_mode": "direct" if "direct" in kname else "ring",
                 "reduce_ms_per_frame": round(r_sum / args.steps, 3),
+                "reduce_ms_meaning": ("the follow-up fold pass only (--pipeline deferred: the part folded inside "
+                                      "the next frame's sample kernel is in kernel_ms, the last frame's flush is "
+                                      "not timed)")
+                if (grouped and args.pipeline == "deferred" and "direct" in kname) else
+                ("direct mode's reduce pass" if "direct" in kname else "none (ring mode accumulates in the kernel)"),
             },
             "hbm": {
                 "algorithmic_bytes_per_frame": alg_bytes,

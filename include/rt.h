@@ -134,6 +134,8 @@ int rt_release_cached_contexts(void);
 typedef struct rt_context rt_context;
 
 int rt_context_create(int device, rt_context** out_ctx);
+/* Runs a pending deferred reduce pass, waits for every launch and pass of the context, then frees
+ * it.  Returns the flush's status (the context is freed either way). */
 int rt_context_destroy(rt_context* ctx);
 /* Uploads the Hittable list to the context's device (once per scene). */
 int rt_context_set_scene(rt_context* ctx, const rt_sphere* spheres, size_t n_spheres);
@@ -171,9 +173,10 @@ int rt_render_rows_async_split(rt_context* ctx, const rt_camera* cam, uint32_t o
  * So the output of call k is complete on ITS out_stream once call k+1 has been issued and its
  * out_stream reaches that point, or after rt_context_flush(ctx) / rt_context_sync(ctx), which run a
  * pending pass whole.  A call that cannot fold the pending pass (a plain or ring-mode call, another
- * launch size) runs it first.  Ring-mode calls behave as rt_render_rows_async_split.  out_stream
- * (NULL: the HIP null stream) must differ from stream.  A caller that destroys the context with a pass pending gets no output
- * for that call. */
+ * launch size, or another out_stream than the pending call's) runs it first.  Ring-mode calls behave
+ * as rt_render_rows_async_split.  out_stream (NULL: the HIP null stream) must differ from stream.
+ * rt_context_destroy runs a pending pass and waits for it before freeing anything: the output of
+ * the last deferred call is complete when destroy returns (RT_OK), never dropped. */
 int rt_render_rows_async_deferred(rt_context* ctx, const rt_camera* cam, uint32_t output_format,
                                   uint32_t row0, uint32_t row_step, uint32_t n_rows,
                                   void* d_out, void* d_stats, void* stream, void* out_stream);

@@ -394,10 +394,11 @@ constexpr int32_t kDone = INT32_MIN;  // walk finished (stack entry 0)
 #define RTZIG_REFETCH_K 56
 #endif
 constexpr int kRefetchK = RTZIG_REFETCH_K;
-// Drain mode (RTZIG_DRAIN, default 1): once a wave's claims find the launch's items exhausted, its
-// walks stop suspending for refills (nothing is left to fetch) and its rejection loops run until
-// every lane has its sample instead of kRuvTrips trips per iteration, so the paths still in flight
-// at the end of a launch take fewer loop iterations (the drain tail).  Results unchanged.
+// Drain mode (RTZIG_DRAIN, default 0: an A/B knob, measured within noise and not adopted): once a
+// wave's claims find the launch's items exhausted, its walks stop suspending for refills (nothing is
+// left to fetch) and its rejection loops run until every lane has its sample instead of kRuvTrips
+// trips per iteration, so the paths still in flight at the end of a launch take fewer loop
+// iterations (the drain tail).  Results unchanged.
 #ifndef RTZIG_DRAIN
 #define RTZIG_DRAIN 0
 #endif

@@ -20,6 +20,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
+#include <chrono>
 #include <exception>
 #include <cmath>
 #include <cstdio>
@@ -76,6 +78,33 @@ constexpr uint32_t kLinearMaxSpheres = 8;    // scenes this small walk the list 
 constexpr const char* kStallMsg =
     "render kernel: a wave gave up waiting for a running-sum hand-off (one wait exceeded its bound: 40 s, "
     "scaled with the sphere count for list walks)";
+
+// Phase trace of one rt_render call (diagnostics: RTZIG_TRACE=1 prints one JSON line to stderr).
+// The drop-in's cost in the reference's own usage is one call per process (main.zig:14-36), so its
+// fixed costs — HIP runtime init, context, scene upload, tree training, workspace, code-object load
+// at the first launch — matter as much as the frame; each mark adds the wall time since the
+// previous mark to its phase.  Marks are taken only on the thread that called rt_render (the
+// per-device threads of a multi-GPU call are covered by the mark after they join).
+struct PhaseTrace {
+    std::thread::id tid;
+    std::chrono::steady_clock::time_point t0, last;
+    std::vector<std::pair<std::string, double>> ms;
+};
+PhaseTrace g_trace;                    // written only under g_cache_mu by the tracing rt_render call
+std::atomic<bool> g_trace_on{false};   // read by every mark (context calls of other threads too)
+
+void trace_mark(const char* phase) {
+    if (!g_trace_on.load(std::memory_order_relaxed) || std::this_thread::get_id() != g_trace.tid) return;
+    const auto now = std::chrono::steady_clock::now();
+    const double d = std::chrono::duration<double, std::milli>(now - g_trace.last).count();
+    g_trace.last = now;
+    for (auto& p : g_trace.ms)
+        if (p.first == phase) {
+            p.second += d;
+            return;
+        }
+    g_trace.ms.emplace_back(phase, d);
+}
 
 }  // namespace
 
@@ -412,11 +441,16 @@ int flush_fold(rt_context* ctx) {
 }
 
 // Waits until the device has finished the context's last render (before rewriting its buffers); a
-// pending deferred reduce pass is run first.
+// pending deferred reduce pass is run first.  `done` marks the end of the LAST call only: a reduce
+// pass of an earlier split / deferred call runs on that call's out stream and may still read its
+// per-sample buffer, so the passes' own events are waited for too.
 int quiesce(rt_context* ctx) {
     int rc = flush_fold(ctx);
     if (rc) return rc;
     if (ctx->done_valid) HIP_CHECK(hipEventSynchronize(ctx->done));
+    for (int b = 0; b < 2; b++)
+        if (ctx->reduced_valid[b]) HIP_CHECK(hipEventSynchronize(ctx->reduced[b]));
+    if (ctx->launched_valid) HIP_CHECK(hipEventSynchronize(ctx->launched));
     HIP_CHECK(hipStreamSynchronize(ctx->stream));
     return RT_OK;
 }
@@ -654,8 +688,10 @@ int rt_context_create(int device, rt_context** out_ctx) {
         return RT_ERR_NO_DEVICE;
     }
     HIP_CHECK(hipSetDevice(device));
+    trace_mark("ctx_set_device");
     hipDeviceProp_t prop;
     HIP_CHECK(hipGetDeviceProperties(&prop, device));
+    trace_mark("ctx_device_props");
     if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
         rt_set_last_error(std::string("device is ") + prop.gcnArchName + ", library built for gfx950");
         return RT_ERR_NO_DEVICE;
@@ -670,6 +706,7 @@ int rt_context_create(int device, rt_context** out_ctx) {
     int cus = 0;
     if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
     ctx->sched_lanes = (uint64_t)std::max(cus, 1) * 16 * 64;
+    trace_mark("ctx_streams_events");
     if (e != hipSuccess) {
         const int rc = hip_fail(e, "rt_context_create: stream / event");
         rt_context_destroy(ctx);
@@ -682,8 +719,13 @@ int rt_context_create(int device, rt_context** out_ctx) {
 int rt_context_destroy(rt_context* ctx) {
     if (!ctx) return RT_OK;
     (void)hipSetDevice(ctx->device);
-    if (ctx->done_valid) (void)hipEventSynchronize(ctx->done);
-    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    // a deferred call's pending reduce pass is run, not dropped: its output was promised to the
+    // caller (the reference's render always fills ppm.pixels, camera.zig:125,138); then every
+    // launch and pass that may still use a buffer is waited for before anything is freed
+    const int rc = quiesce(ctx);
+    if (rc) {  // still free what can be freed after a device-wide wait
+        (void)hipDeviceSynchronize();
+    }
     for (void* p : {(void*)ctx->d_geo, (void*)ctx->d_mat, (void*)ctx->d_ring, (void*)ctx->d_sums, (void*)ctx->d_flags,
                     (void*)ctx->d_samples, (void*)ctx->d_samples2, (void*)ctx->d_fold_ctr, (void*)ctx->d_sched, (void*)ctx->d_ctr, (void*)ctx->d_nodes, (void*)ctx->d_leaves, (void*)ctx->d_always_geo,
                     (void*)ctx->d_always_sid, ctx->d_out, (void*)ctx->d_stats})
@@ -695,7 +737,7 @@ int rt_context_destroy(rt_context* ctx) {
         if (e) (void)hipEventDestroy(e);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
-    return RT_OK;
+    return rc;  // a failed flush: the context is gone, the pending output may be incomplete
 }
 
 int rt_context_set_scene(rt_context* ctx, const rt_sphere* spheres, size_t n) {
@@ -767,15 +809,19 @@ int render_rows(rt_context* ctx, const rt_camera* cam, uint32_t output_format, u
         build_bvh(ctx->scene, std::max(cam_bound, ctx->scene.origin_bound) * 1.01);
         rc = upload_bvh(ctx);
         if (rc) return rc;
+        trace_mark("bvh_rebuild_far_camera");
     }
     // large launches walk a tree trained on this camera's rays (same bits, fewer node visits)
     if (want_train(ctx->scene, (uint64_t)n_rows * cam->image_width * cam->samples_per_pixel) &&
         !(ctx->scene.train_tried && same_view(ctx->scene.view, *cam))) {
         rc = quiesce(ctx);  // the previous render may still walk the old tree
         if (rc) return rc;
+        trace_mark("wait_previous_render");
         train_bvh(ctx->scene, *cam);
+        trace_mark("bvh_train_host");
         rc = upload_bvh(ctx);
         if (rc) return rc;
+        trace_mark("bvh_upload");
     }
 
     const uint64_t P = (uint64_t)n_rows * cam->image_width;
@@ -784,6 +830,7 @@ int render_rows(rt_context* ctx, const rt_camera* cam, uint32_t output_format, u
     const uint64_t n_tiles = (P + 63) / 64;
     rc = upload_schedule(ctx, cam->samples_per_pixel, P);
     if (rc) return rc;
+    trace_mark("schedule_upload");
     ua.chunk_s0 = ctx->d_sched;
     ua.n_chunks = (uint32_t)(ctx->sched.size() - 1);
     if (n_tiles * ua.n_chunks >= (1ull << 32)) {
@@ -822,9 +869,12 @@ int render_rows(rt_context* ctx, const rt_camera* cam, uint32_t output_format, u
     // deferred calls (direct mode, an output stream): this call's reduce pass is left pending for the
     // next deferred call's drained waves; a pending pass this call will not fold (a plain or ring-mode
     // call, another launch size) runs whole first
+    // The pending pass's follow-up fold runs on this call's out stream, so it is folded only when
+    // that is the stream the pending output was promised on (a consumer that queued work there after
+    // this call is then ordered after the fold); otherwise it runs whole on its own stream first.
     const bool defer_fold = defer && direct && split;
     if (ctx->fold_pending && !(defer_fold && ctx->fold.P == (uint32_t)P && ctx->fold.spp == cam->samples_per_pixel &&
-                               ctx->fold_buf == (ctx->samples_flip ^ 1u))) {
+                               ctx->fold_buf == (ctx->samples_flip ^ 1u) && ctx->fold_stream == os)) {
         rc = flush_fold(ctx);
         if (rc) return rc;
     }
@@ -873,6 +923,7 @@ int render_rows(rt_context* ctx, const rt_camera* cam, uint32_t output_format, u
         if (!rc) HIP_CHECK(hipMemsetAsync(ctx->d_ctr, 0, rtk::kCtrBytes, s));
     }
     if (rc) return rc;
+    trace_mark("workspace_alloc");
     ua.ring = direct ? nullptr : ctx->d_ring;
     ua.sums = direct ? nullptr : ctx->d_sums;
     ua.samples = direct ? (sbuf ? ctx->d_samples2 : ctx->d_samples) : nullptr;
@@ -922,7 +973,9 @@ int render_rows(rt_context* ctx, const rt_camera* cam, uint32_t output_format, u
     if (!direct) HIP_CHECK(hipMemsetAsync(ctx->d_flags, 0, flag_bytes, s));
     hipEvent_t* ev = ctx->timing ? &ctx->events[kEventsPerCall * ctx->call_first] : nullptr;
     if (ev) HIP_CHECK(hipEventRecord(ev[0], s));
+    trace_mark("launch_setup");
     HIP_CHECK(launch(&ua, nullptr));
+    trace_mark("launch_issue");
     if (ev) HIP_CHECK(hipEventRecord(ev[1], s));
     HIP_CHECK(hipEventRecord(ctx->launched, s));
     ctx->launched_valid = true;
@@ -1115,6 +1168,32 @@ int device_map(std::vector<int>& map) {
     return RT_OK;
 }
 
+// RTZIG_TRACE=1: starts g_trace for one rt_render call and prints it when the call returns
+struct TraceScope {
+    std::vector<double> kernel_ms;  // HIP-event sample-kernel time per device
+    TraceScope() {
+        const char* e = std::getenv("RTZIG_TRACE");
+        if (!(e && *e && std::strcmp(e, "0") != 0)) return;
+        g_trace = PhaseTrace{};
+        g_trace.tid = std::this_thread::get_id();
+        g_trace.t0 = g_trace.last = std::chrono::steady_clock::now();
+        g_trace_on = true;
+    }
+    ~TraceScope() {
+        if (!g_trace_on) return;
+        trace_mark("return");
+        const double total = std::chrono::duration<double, std::milli>(g_trace.last - g_trace.t0).count();
+        std::string j = "{\"rt_render_trace\": {\"total_ms\": " + std::to_string(total) + ", \"phases_ms\": {";
+        for (size_t i = 0; i < g_trace.ms.size(); i++)
+            j += (i ? ", \"" : "\"") + g_trace.ms[i].first + "\": " + std::to_string(g_trace.ms[i].second);
+        j += "}, \"kernel_ms\": [";
+        for (size_t i = 0; i < kernel_ms.size(); i++) j += (i ? ", " : "") + std::to_string(kernel_ms[i]);
+        j += "]}}\n";
+        std::fputs(j.c_str(), stderr);
+        g_trace_on = false;
+    }
+};
+
 // Gets (creating if needed) the cached contexts of devices [first, first + G) and makes each hold
 // `spheres`: contexts are created on parallel host threads; the scene is built on the host once
 // per call at most and uploaded only where it differs.
@@ -1132,6 +1211,7 @@ int cached_contexts(const std::vector<int>& map, int first, int G, const rt_sphe
     }
     SceneData sd;
     if (need_scene) build_scene(spheres, n, sd);
+    trace_mark("scene_build_host");
     std::vector<int> rcs(G, RT_OK);
     std::vector<std::string> msgs(G);
     auto work = [&](int g) {
@@ -1139,6 +1219,7 @@ int cached_contexts(const std::vector<int>& map, int first, int G, const rt_sphe
         int rc = RT_OK;
         if (!c) rc = rt_context_create(map[first + g], &c);
         if (!rc && !same_spheres(c->scene, spheres, n)) rc = upload_scene(c, sd);
+        trace_mark("scene_upload");
         rcs[g] = rc;
         if (rc) msgs[g] = rt_last_error();  // thread-local: carried back to the caller's thread
     };
@@ -1148,6 +1229,7 @@ int cached_contexts(const std::vector<int>& map, int first, int G, const rt_sphe
         std::vector<std::thread> th;
         for (int g = 0; g < G; g++) th.emplace_back(work, g);
         for (auto& t : th) t.join();
+        trace_mark("contexts_on_device_threads");
     }
     for (int g = 0; g < G; g++)
         if (rcs[g]) {
@@ -1180,9 +1262,12 @@ int rt_render(const rt_camera* cam, const rt_sphere* spheres, size_t n, const rt
         rt_set_last_error("pixel_stride must be >= 3");
         return RT_ERR_INVALID;
     }
+    std::lock_guard<std::mutex> lock(g_cache_mu);  // also guards g_trace
+    TraceScope trace;
     std::vector<int> map;
-    rc = device_map(map);
+    rc = device_map(map);  // the process's first HIP call initialises the runtime
     if (rc) return rc;
+    trace_mark("hip_init_device_map");
     const int count = (int)map.size();
     const int first = o.device;
     int G = o.n_gpus > 0 ? o.n_gpus : count - first;
@@ -1194,10 +1279,11 @@ int rt_render(const rt_camera* cam, const rt_sphere* spheres, size_t n, const rt
     G = std::min<int>(G, (int)H);
     const size_t px_bytes = o.output_format == RT_OUT_LINEAR_F64 ? 3 * sizeof(double) : 3;
 
-    std::lock_guard<std::mutex> lock(g_cache_mu);
     std::vector<rt_context*> ctxs;
     rc = cached_contexts(map, first, G, spheres, n, ctxs);
     if (rc) return rc;
+    if (g_trace_on)
+        for (rt_context* c : ctxs) (void)rt_context_enable_timing(c, 1);
     std::vector<uint32_t> rows(G);
     for (int g = 0; g < G; g++) {
         rt_context* c = ctxs[g];
@@ -1219,6 +1305,7 @@ int rt_render(const rt_camera* cam, const rt_sphere* spheres, size_t n, const rt
             c->h_out_bytes = bytes;
         }
         if (!c->h_stats) HIP_CHECK(hipHostMalloc((void**)&c->h_stats, 3 * sizeof(uint64_t), hipHostMallocDefault));
+        trace_mark("output_staging_alloc");
         HIP_CHECK(hipMemsetAsync(c->d_stats, 0, 2 * sizeof(uint64_t), c->stream));
         rc = rt_render_rows_async(c, cam, o.output_format, (uint32_t)g, (uint32_t)G, rows[g], c->d_out, c->d_stats,
                                   c->stream);
@@ -1226,6 +1313,7 @@ int rt_render(const rt_camera* cam, const rt_sphere* spheres, size_t n, const rt
         HIP_CHECK(hipMemcpyAsync(c->h_out, c->d_out, bytes, hipMemcpyDeviceToHost, c->stream));
         HIP_CHECK(hipMemcpyAsync(c->h_stats, c->d_stats, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
         HIP_CHECK(hipMemcpyAsync(c->h_stats + 2, c->d_ctr + rtk::kErrWord, sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
+        trace_mark("copies_issue");
     }
     // Wait for each device and un-interleave its rows j = g + k*G into the caller's framebuffer, one
     // host thread per device (at 8 GPUs the 23 MB host copy would otherwise rival the render).
@@ -1236,6 +1324,7 @@ int rt_render(const rt_camera* cam, const rt_sphere* spheres, size_t n, const rt
         rt_context* c = ctxs[g];
         hipError_t e = hipSetDevice(c->device);
         if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+        trace_mark("device_wait_kernel_and_d2h");
         if (e != hipSuccess) {
             rcs[g] = hip_fail(e, "rt_render: device work");
             msgs[g] = rt_last_error();  // thread-local: carried back to the caller's thread
@@ -1270,11 +1359,19 @@ int rt_render(const rt_camera* cam, const rt_sphere* spheres, size_t n, const rt
     };
     if (G == 1) {
         collect(0);
+        trace_mark("uninterleave_to_caller");
     } else {
         std::vector<std::thread> th;
         for (int g = 0; g < G; g++) th.emplace_back(collect, g);
         for (auto& t : th) t.join();
+        trace_mark("device_wait_and_uninterleave_threads");
     }
+    if (g_trace_on)
+        for (rt_context* c : ctxs) {
+            double k = 0;
+            if (rt_context_kernel_times(c, &k, nullptr) == RT_OK) trace.kernel_ms.push_back(k);
+            (void)rt_context_enable_timing(c, 0);
+        }
     uint64_t stats[2] = {0, 0};
     for (int g = 0; g < G; g++) {
         if (rcs[g]) {

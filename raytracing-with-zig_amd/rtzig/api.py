@@ -266,9 +266,10 @@ class DeviceRenderer:
         return a.value, b.value, n.value
 
     def close(self):
+        """rt_context_destroy: runs a pending deferred reduce pass and waits for every launch first."""
         if self.ctx:
-            self.lib.rt_context_destroy(self.ctx)
-            self.ctx = C.c_void_p()
+            ctx, self.ctx = self.ctx, C.c_void_p()
+            check("rt_context_destroy", self.lib.rt_context_destroy(ctx))
 
     def __del__(self):
         try:

@@ -766,3 +766,61 @@ def test_split_and_deferred_on_the_null_stream(oracle, monkeypatch):
     r.close()
     for img in got:
         assert np.array_equal(img.cpu().numpy(), ref)
+
+
+def test_destroy_completes_pending_deferred_output(oracle, monkeypatch):
+    """rt_context_destroy with a deferred call's reduce pass still pending runs the pass and waits
+    for it before freeing the context: the output is complete and bit-exact against oracle B once
+    destroy returns (the reference's render always fills ppm.pixels, camera.zig:125,138)."""
+    import torch
+    monkeypatch.setenv("RTZIG_UNIT_MODE", "direct")
+    cam = rtzig.final_scene_camera(width=1200, aspect_ratio=1.5, spp=24)
+    ref, rays = oracle.render_b(cam.cam, cam.scene.world, row0=3, row_step=8, n_rows=12, threads=16)
+    r = rtzig.DeviceRenderer(0)
+    r.set_scene(cam.scene.world)
+    render, coll = torch.cuda.Stream(), torch.cuda.Stream()
+    out = torch.zeros((12, 1200, 3), dtype=torch.float64, device="cuda:0")
+    stats = torch.zeros(2, dtype=torch.int64, device="cuda:0")
+    r.render_rows_async(cam.cam, out.data_ptr(), row0=3, row_step=8, n_rows=12, d_stats_ptr=stats.data_ptr(),
+                        stream_ptr=render.cuda_stream, out_stream_ptr=coll.cuda_stream, deferred=True)
+    assert r.fold_pending()
+    r.close()  # destroy: must flush, not drop
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy(), ref)
+    assert stats.cpu().tolist() == [rays, 12 * 1200 * 24]
+
+
+def test_deferred_alternating_out_streams(oracle, monkeypatch):
+    """Consecutive deferred calls on DIFFERENT out streams: the pending pass of call k is promised on
+    call k's out stream, so call k+1 (another out stream) must not fold it on its own stream — it runs
+    the pass whole on call k's stream first.  Each frame is read on its own out stream right after the
+    next call is issued (rt.h's contract), four frames, every one bit-exact against oracle B."""
+    import torch
+    monkeypatch.setenv("RTZIG_UNIT_MODE", "direct")
+    cam = rtzig.final_scene_camera(width=1200, aspect_ratio=1.5, spp=24)
+    ref, _ = oracle.render_b(cam.cam, cam.scene.world, row0=6, row_step=8, n_rows=12, threads=16)
+    r = rtzig.DeviceRenderer(0)
+    r.set_scene(cam.scene.world)
+    render = torch.cuda.Stream()
+    outs_s = [torch.cuda.Stream(), torch.cuda.Stream()]
+    outs = [torch.zeros((12, 1200, 3), dtype=torch.float64, device="cuda:0") for _ in range(2)]
+    got = []
+    for k in range(4):
+        for s in outs_s:
+            render.wait_stream(s)  # the clones below have read the buffer this call may write
+        r.render_rows_async(cam.cam, outs[k % 2].data_ptr(), row0=6, row_step=8, n_rows=12,
+                            stream_ptr=render.cuda_stream, out_stream_ptr=outs_s[k % 2].cuda_stream, deferred=True)
+        if k:
+            with torch.cuda.stream(outs_s[(k - 1) % 2]):
+                got.append(outs[(k - 1) % 2].clone())  # frame k-1: complete on ITS out stream now
+    r.flush()
+    with torch.cuda.stream(outs_s[3 % 2]):
+        got.append(outs[3 % 2].clone())
+    for s in outs_s:
+        s.synchronize()
+    imgs = [g.cpu().numpy() for g in got]
+    r.sync()
+    r.close()
+    assert len(imgs) == 4
+    for img in imgs:
+        assert np.array_equal(img, ref)

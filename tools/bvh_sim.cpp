@@ -203,7 +203,16 @@ int main(int argc, char** argv) {
             auto cell = [](double v) { return (uint64_t)std::min(15.0, std::max(0.0, (v + 16) / 2)); };
             const uint64_t c = cell(r.o.x) | cell(r.o.y) << 4 | cell(r.o.z) << 8;
             if (key_mode == 1) return oct << 12 | c;
-            return c << 3 | oct;
+            if (key_mode == 2) return c << 3 | oct;
+            // scalar keys: the unit direction's y (up-going rays leave the clutter sooner), the
+            // origin's height, camera vs secondary
+            const double uy = r.d.y / std::sqrt(dot(r.d, r.d));
+            const uint64_t ybin = (uint64_t)std::min(15.0, std::max(0.0, (uy + 1) * 8));
+            const uint64_t hbin = (uint64_t)std::min(7.0, std::max(0.0, r.o.y * 4 + 1));
+            if (key_mode == 3) return ybin;
+            if (key_mode == 4) return hbin << 4 | ybin;
+            if (key_mode == 5) return (uint64_t)r.camera << 8 | hbin << 4 | ybin;
+            return (uint64_t)r.camera << 16 | oct << 8 | hbin << 4 | ybin;
         };
         for (size_t b = 0; b + group <= rays.size(); b += group)
             std::stable_sort(rays.begin() + b, rays.begin() + b + group,
@@ -222,6 +231,7 @@ int main(int argc, char** argv) {
     const bool skip_leaf_only = std::getenv("SIM_SKIP_DEAD_LEAF_ONLY") != nullptr;  // ... only after a leaf round
     double dead = 0;
     size_t nw = 0;
+    std::vector<int> ray_visits(rays.size(), 0);  // inner steps of each ray's walk (SIM_GROUP_ORACLE)
     for (size_t w0 = 0; w0 + 64 <= rays.size(); w0 += 64, ++nw) {
         size_t maxleaf = 0;
         for (int l = 0; l < 64; l++) {
@@ -294,6 +304,7 @@ int main(int argc, char** argv) {
                 }
             }
             runs[l].push_back(run);
+            for (int v : runs[l]) ray_visits[w0 + l] += v;
             maxleaf = std::max(maxleaf, runs[l].size() - 1);
         }
         wave_leaf += (double)maxleaf;
@@ -304,6 +315,22 @@ int main(int argc, char** argv) {
             wave_steps += m;
         }
     }
+    // optional (upper bound of ANY regrouping key): SIM_GROUP_ORACLE=g sorts each batch of g
+    // consecutive rays by their true walk length (inner steps, known only after the walk) before the
+    // wave models below, as if a block could group its in-flight segments by the cost they are
+    // about to have
+    if (const char* e = std::getenv("SIM_GROUP_ORACLE")) {
+        const size_t group = (size_t)std::atoi(e);
+        std::vector<size_t> idx(rays.size());
+        for (size_t i = 0; i < idx.size(); i++) idx[i] = i;
+        for (size_t b = 0; b + group <= rays.size(); b += group)
+            std::stable_sort(idx.begin() + b, idx.begin() + b + group,
+                             [&](size_t x, size_t y) { return ray_visits[x] < ray_visits[y]; });
+        std::vector<Ray> sorted(rays.size());
+        for (size_t i = 0; i < idx.size(); i++) sorted[i] = rays[idx[i]];
+        rays.swap(sorted);
+    }
+
     // ---- lockstep model of one wave (SIM_LOCKSTEP): all lanes advance together; with SIM_STEAL a
     // lane whose walk is over takes the oldest stack entry of the lane with the deepest stack and
     // walks that subtree for the same ray (closest shared instantly: an optimistic bound) ----
