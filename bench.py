@@ -20,8 +20,10 @@ strong scaling.  Rank 0 prints ONE JSON line.
 `roofline` is the dominant kernel's VALU roofline (bound "valu": no GEMM-shaped work on this path,
 DESIGN.md §5): achieved = the FLOPs the sample kernel executes per frame (exact in-kernel counts of
 one instrumented frame: 17 f64 FLOPs per ray-sphere candidate test, SURVEY §8(d)'s unit, plus 24 f32
-FLOPs per BVH node visit counted at half weight) / its HIP-event time, against the 78.6 TFLOP/s FP64
-vector peak.  `roofline.issue` is the VALU-issue cycle model from the committed PMC summary.
+FLOPs per BVH node visit counted at half weight: a packed f32 fma issues in the cycles of one f64 fma)
+/ its HIP-event time, against the 78.6 TFLOP/s FP64 vector peak (69.3 measured, profiles/r05_peak/).
+`roofline.issue` is the VALU-issue cycle model from the committed PMC summary (event-timed issue costs
+per opcode and operand form): the kernel is VALU-issue-bound, so that fraction is the one that binds.
 `cpu_baseline` times the oracle's sequential-stream port of the reference (single thread — the
 reference's single RNG stream is inherently sequential) on a bounded sample of the same frame.
 """
@@ -44,7 +46,10 @@ import rtzig  # noqa: E402
 from rtzig import dist as rdist  # noqa: E402
 
 METRIC = "Msamples/sec (pixels×spp/s) on final-render scene; achieved HBM GB/s vs peak"
-FP64_VALU_PEAK_TFLOPS = 78.6   # MI355X vector FP64 (spec) = unpacked FP32 at half weight
+FP64_VALU_PEAK_TFLOPS = 78.6   # MI355X vector FP64 (spec): 16 lanes/clock/SIMD at 2.4 GHz
+# the same measured with hipEvents over all CUs (v_fma_f64, 8 waves/SIMD, the chip at 2.20 GHz under
+# that load): profiles/r05_peak/ (round 4's 2.12-cycle s_memtime rate was a residency artefact)
+FP64_VALU_MEASURED_TFLOPS = 69.3
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E (spec), MI355X_MICROARCH.md
 SIMDS = 1024                   # 256 CUs x 4 SIMDs
 FLOPS_PER_TEST = 17            # oc(3) + h(5) + |oc|^2(5) + -r^2(1) + h^2-a*c(3), SURVEY §8(d)
@@ -465,9 +470,10 @@ def run(args):
             cyc = pmc["valu_issue_cycles_per_frame"]
             issue = {"frac": round(cyc / (SIMDS * pmc["clock_GHz"] * 1e9 * k_frame_s), 4),
                      "valu_issue_cycles_per_frame": cyc, "clock_GHz": pmc["clock_GHz"],
-                     "model": "PMC VALU counts x issue cycles per wave64 instruction MEASURED on the MI355X at "
-                              "4 waves/SIMD (f64 add/mul/fma 2.12, rsq/rcp_f64 7.94, rcp_f32 6.03, the other "
-                              "ops at the kernel's own measured-rate mix), / (1024 SIMDs x clock x kernel time)",
+                     "model": "PMC VALU counts x issue cycles per wave64 instruction MEASURED on the MI355X with "
+                              "hipEvent timing (f64 add/mul/fma 4.17, rsq/rcp_f64 16.1, f32 transcendentals 8.1, "
+                              "the other ops at the kernel's own operand-aware mix of 4.15-cycle and 2.2-cycle "
+                              "forms), / (1024 SIMDs x clock x kernel time): the bound that binds",
                      "rates": pmc.get("valu_issue_model"),
                      "source": pmc.get("source")}
         # HBM: the algorithmic traffic of a frame is the f64 linear framebuffer W*H*24 (or W*H*3
@@ -514,6 +520,11 @@ def run(args):
                 "peak": FP64_VALU_PEAK_TFLOPS,
                 "unit": "TFLOP/s",
                 "frac": round(exec_tf / FP64_VALU_PEAK_TFLOPS, 4),
+                "peak_measured": {"TFLOP/s": FP64_VALU_MEASURED_TFLOPS,
+                                  "frac": round(exec_tf / FP64_VALU_MEASURED_TFLOPS, 4),
+                                  "source": "profiles/r05_peak/ (tools/peak_rates.hip: event-timed v_fma_f64 over "
+                                            "all CUs; 4.16 SIMD cycles per wave64 instruction = the spec's "
+                                            "16 lanes/clock at the 2.2 GHz the chip holds under that load)"},
                 "traffic": traffic,
                 "work": f"executed per frame (rank 0, {n_rows} rows; exact counts of one instrumented frame): "
                         f"{tests} f64 ray-sphere tests x {FLOPS_PER_TEST} FLOP (SURVEY §8(d) unit) + "

@@ -1364,20 +1364,19 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
             const double l = sqrt_normal(uls);  // |p|^2 in (1e-160, 1] (vec.zig:76)
             const SharedRcp rl(l);
             const v3 ruv = mk(rl.div(ux), rl.div(uy), rl.div(uz));  // p / sqrt(|p|^2), true divisions
-            v3 dir;
+            // the new direction is written in place: an absorbed ray's direction is never read again
             bool absorbed = false;
             if (!sc_metal) {
-                dir = sc_nrm + ruv;
-                if (near_zero(dir)) dir = sc_nrm;
+                r.dir = sc_nrm + ruv;
+                if (near_zero(r.dir)) r.dir = sc_nrm;
             } else {
-                dir = sc_refl + muls(ruv, sc_fuzz);  // unit(reflect(ray.dir, n)) + fuzz * ruv
-                absorbed = !(dot(dir, sc_nrm) > 0);  // absorbed -> black
+                r.dir = sc_refl + muls(ruv, sc_fuzz);  // unit(reflect(ray.dir, n)) + fuzz * ruv
+                absorbed = !(dot(r.dir, sc_nrm) > 0);  // absorbed -> black
             }
             pending = false;
             if (absorbed) {
                 done = true;
             } else {
-                r.dir = dir;
                 ++bounce;
             }
         }
@@ -1434,37 +1433,37 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
                 // dielectric (unit(ray.dir)) and the metal (unit(reflect(ray.dir, n))).  Each is a
                 // correctly rounded sqrt and division, and a wave executes every branch some lane
                 // takes; so each lane selects its vector first and one unit() serves all three.
-                // The hit record and material are read only by lanes with a hit (k >= 0).  They start
-                // as arbitrary values (__builtin_nondeterministic_value: no instruction), not zeros:
-                // zero-initialized, they cost ~15 v_mov per iteration for the sky lanes.
-                v3 pt = mk(__builtin_nondeterministic_value(0.0), __builtin_nondeterministic_value(0.0),
-                           __builtin_nondeterministic_value(0.0));
-                v3 nrm = mk(__builtin_nondeterministic_value(0.0), __builtin_nondeterministic_value(0.0),
-                            __builtin_nondeterministic_value(0.0));
-                v3 alb = mk(__builtin_nondeterministic_value(0.0), __builtin_nondeterministic_value(0.0),
-                            __builtin_nondeterministic_value(0.0));
-                double fuzz = __builtin_nondeterministic_value(0.0), ri = __builtin_nondeterministic_value(0.0),
-                       r0 = __builtin_nondeterministic_value(0.0);
-                uint32_t kind = __builtin_nondeterministic_value(0u);
-                v3 x = r.dir;
+                // The hit record and material are computed by EVERY shaded lane, the sky lanes on
+                // sphere 0's records (their values are never used): a wave runs this block whenever
+                // any lane hit, so the sky lanes cost no extra issue, and without the divergent
+                // `if (k >= 0)` there is no merge of the hit values with placeholder ones (the
+                // compiler zeroed 12 registers per iteration for it, and copied ray.dir).
                 if (k >= 0 && !bounds_ok((uint32_t)k < p.n_spheres, ua.ctr)) k = -1;
-                if (k >= 0) {
-                    const GeoRec sg = geo_orig[k];
-                    const MatRec m = mat_g[k];
-                    // hit record (sphere.zig:44-53)
-                    pt = r.orig + muls(r.dir, t);
-                    const v3 outward = muls(pt - mk(sg.cx, sg.cy, sg.cz), m.inv_r);
-                    const bool front = dot(r.dir, outward) < 0;
-                    nrm = front ? outward : -outward;
-                    kind = m.kind;
-                    alb = mk(m.albedo[0], m.albedo[1], m.albedo[2]);
-                    fuzz = m.fuzz;
-                    ri = front ? m.inv_ior : m.ior;        // dielectric: 1.0 / ior precomputed (same bits)
-                    r0 = front ? m.r0_front : m.r0_back;   // Schlick ((1-ri)/(1+ri))^2, host
-                    if (kind == 1) x = reflect(r.dir, nrm);
-                }
-                const v3 u = unit(x);
-                if (k < 0) {
+                const bool hit = k >= 0;
+                const uint32_t kk = hit ? (uint32_t)k : 0u;
+                const GeoRec sg = geo_orig[kk];
+                const MatRec m = mat_g[kk];
+                // hit record (sphere.zig:44-53); a sky lane's t is t_max (inf): its values are unused
+                const v3 pt = r.orig + muls(r.dir, t);
+                const v3 outward = muls(pt - mk(sg.cx, sg.cy, sg.cz), m.inv_r);
+                const bool front = dot(r.dir, outward) < 0;
+                const v3 nrm = front ? outward : -outward;
+                const uint32_t kind = m.kind;
+                const double ri = front ? m.inv_ior : m.ior;        // dielectric: 1.0 / ior precomputed (same bits)
+                const double r0 = front ? m.r0_front : m.r0_back;   // Schlick ((1-ri)/(1+ri))^2, host
+                // a metal lane's ray.dir is not read again before its scatter finishes (it then
+                // takes sc_refl + fuzz * ruv), so the reflected direction replaces it in place
+                if (hit && kind == 1) r.dir = reflect(r.dir, nrm);
+                const v3 u = unit(r.dir);
+                // The scatter state is read only while `pending`, and a shaded lane was not
+                // pending: every shaded lane takes it (and the hit point as its next origin; a sky
+                // lane's path ends here), so these are plain writes, not copies under a branch.
+                sc_nrm = nrm;
+                sc_refl = u;
+                sc_fuzz = m.fuzz;
+                sc_metal = kind == 1;
+                r.orig = pt;
+                if (!hit) {
                     // sky gradient (camera.zig:171-177)
                     const double a = 0.5 * (u.y + 1.0);
                     const v3 sky = muls(mk(1, 1, 1), 1.0 - a) + muls(mk(0.5, 0.7, 1), a);
@@ -1474,13 +1473,8 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
                     // Lambertian (material.zig:27-39) / Metal (:55-68): attenuation = albedo.  A
                     // metal ray that ends up absorbed returns black whatever `att` is, so the
                     // product can be taken now.
-                    att = att * alb;
+                    att = att * mk(m.albedo[0], m.albedo[1], m.albedo[2]);
                     pending = true;
-                    sc_metal = kind == 1;
-                    sc_fuzz = fuzz;
-                    sc_nrm = nrm;
-                    sc_refl = u;
-                    r.orig = pt;
                 } else {  // Dielectric.scatter (material.zig:82-110), attenuation (1,1,1)
                     const v3 ud = u;
                     const double cos_t = __builtin_fmin(dot(-ud, nrm), 1.0);
@@ -1489,7 +1483,6 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
                     const double approx = r0 + (1 - r0) * zig_pow5(1 - cos_t);
                     // short-circuit `or` (material.zig:94): draw only if refraction is possible
                     const v3 dir = (cannot || approx > g.uniform()) ? reflect(ud, nrm) : refract(ud, nrm, ri);
-                    r.orig = pt;
                     r.dir = dir;
                     ++bounce;
                 }

@@ -23,6 +23,7 @@
 #include <atomic>
 #include <chrono>
 #include <exception>
+#include <functional>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -104,6 +105,12 @@ void trace_mark(const char* phase) {
             return;
         }
     g_trace.ms.emplace_back(phase, d);
+}
+
+// a duration measured elsewhere (a host thread), reported under its own name
+void trace_note(const char* name, double ms) {
+    if (!g_trace_on.load(std::memory_order_relaxed) || std::this_thread::get_id() != g_trace.tid) return;
+    g_trace.ms.emplace_back(std::string("[") + name + "]", ms);
 }
 
 }  // namespace
@@ -370,6 +377,31 @@ bool try_train(SceneData& sd, const rt_camera& cam) {
     }
     sd = tr;
     return true;
+}
+
+// The tree preparation a launch of `samples` samples with camera `cam` does before it runs
+// (render_rows): a rebuild with a larger origin bound when the camera's ray origins lie beyond it,
+// then the ray-driven training.  Host work only; rt_render runs it on a host thread while the HIP
+// runtime and the contexts initialise, so render_rows finds nothing left to do.
+double cam_origin_bound(const rt_camera& cam) {
+    double b = 0;
+    for (int a = 0; a < 3; a++)
+        b = std::max(b, std::fabs(cam.center[a]) + std::fabs(cam.defocus_disk_u[a]) + std::fabs(cam.defocus_disk_v[a]));
+    return b;
+}
+bool needs_far_rebuild(const SceneData& sd, const rt_camera& cam) {
+    return sd.bvh_ok && !(cam_origin_bound(cam) <= sd.origin_bound);
+}
+double far_bound(const SceneData& sd, const rt_camera& cam) {
+    return std::max(cam_origin_bound(cam), sd.origin_bound) * 1.01;
+}
+bool needs_training(const SceneData& sd, const rt_camera& cam, uint64_t samples) {
+    return want_train(sd, samples) && !(sd.train_tried && same_view(sd.view, cam));
+}
+void train_bvh(SceneData& sd, const rt_camera& cam);
+void prepare_tree(SceneData& sd, const rt_camera& cam, uint64_t samples) {
+    if (needs_far_rebuild(sd, cam)) build_bvh(sd, far_bound(sd, cam));
+    if (needs_training(sd, cam, samples)) train_bvh(sd, cam);
 }
 
 void train_bvh(SceneData& sd, const rt_camera& cam) {
@@ -799,21 +831,16 @@ int render_rows(rt_context* ctx, const rt_camera* cam, uint32_t output_format, u
 
     // camera-ray origins (center + defocus disk) must lie inside the BVH padding's origin bound
     // (lanes outside it would walk without culling: correct, but every camera ray would pay)
-    double cam_bound = 0;
-    for (int a = 0; a < 3; a++)
-        cam_bound = std::max(cam_bound, std::fabs(cam->center[a]) + std::fabs(cam->defocus_disk_u[a]) +
-                                            std::fabs(cam->defocus_disk_v[a]));
-    if (ctx->scene.bvh_ok && !(cam_bound <= ctx->scene.origin_bound)) {
+    if (needs_far_rebuild(ctx->scene, *cam)) {
         rc = quiesce(ctx);  // the previous render may still walk the old tree
         if (rc) return rc;
-        build_bvh(ctx->scene, std::max(cam_bound, ctx->scene.origin_bound) * 1.01);
+        build_bvh(ctx->scene, far_bound(ctx->scene, *cam));
         rc = upload_bvh(ctx);
         if (rc) return rc;
         trace_mark("bvh_rebuild_far_camera");
     }
     // large launches walk a tree trained on this camera's rays (same bits, fewer node visits)
-    if (want_train(ctx->scene, (uint64_t)n_rows * cam->image_width * cam->samples_per_pixel) &&
-        !(ctx->scene.train_tried && same_view(ctx->scene.view, *cam))) {
+    if (needs_training(ctx->scene, *cam, (uint64_t)n_rows * cam->image_width * cam->samples_per_pixel)) {
         rc = quiesce(ctx);  // the previous render may still walk the old tree
         if (rc) return rc;
         trace_mark("wait_previous_render");
@@ -1197,39 +1224,65 @@ struct TraceScope {
 // Gets (creating if needed) the cached contexts of devices [first, first + G) and makes each hold
 // `spheres`: contexts are created on parallel host threads; the scene is built on the host once
 // per call at most and uploaded only where it differs.
+// `scene()` returns the host scene (built on first use; rt_render hands in one built and
+// tree-prepared on a host thread meanwhile), called only if some context needs it, before any
+// upload and on the calling thread.
 int cached_contexts(const std::vector<int>& map, int first, int G, const rt_sphere* spheres, size_t n,
-                    std::vector<rt_context*>& out) {
+                    const std::function<const SceneData&()>& scene, std::vector<rt_context*>& out) {
     if ((int)g_cache.size() < first + G) g_cache.resize(first + G, nullptr);
-    bool need_scene = false;
     for (int g = 0; g < G; g++) {
         rt_context*& c = g_cache[first + g];
         if (c && c->device != map[first + g]) {  // the logical -> physical map changed
             rt_context_destroy(c);
             c = nullptr;
         }
-        need_scene = need_scene || !c || !same_spheres(c->scene, spheres, n);
     }
-    SceneData sd;
-    if (need_scene) build_scene(spheres, n, sd);
-    trace_mark("scene_build_host");
     std::vector<int> rcs(G, RT_OK);
     std::vector<std::string> msgs(G);
-    auto work = [&](int g) {
+    const SceneData* sd = nullptr;
+    auto create = [&](int g) {
         rt_context*& c = g_cache[first + g];
         int rc = RT_OK;
         if (!c) rc = rt_context_create(map[first + g], &c);
-        if (!rc && !same_spheres(c->scene, spheres, n)) rc = upload_scene(c, sd);
-        trace_mark("scene_upload");
         rcs[g] = rc;
         if (rc) msgs[g] = rt_last_error();  // thread-local: carried back to the caller's thread
     };
+    auto work = [&](int g) {
+        rt_context* c = g_cache[first + g];
+        int rc = RT_OK;
+        if (!same_spheres(c->scene, spheres, n)) rc = upload_scene(c, *sd);
+        trace_mark("scene_upload");
+        rcs[g] = rc;
+        if (rc) msgs[g] = rt_last_error();
+    };
+    // 1. contexts (the first stream of a process costs ~20 ms: HIP queue creation)
     if (G == 1) {
+        create(0);
+    } else {
+        std::vector<std::thread> th;
+        for (int g = 0; g < G; g++) th.emplace_back(create, g);
+        for (auto& t : th) t.join();
+        trace_mark("contexts_on_device_threads");
+    }
+    for (int g = 0; g < G; g++)
+        if (rcs[g]) {
+            rt_set_last_error(msgs[g]);
+            return rcs[g];
+        }
+    // 2. the scene, where a context does not hold it yet
+    bool need_scene = false;
+    for (int g = 0; g < G; g++) need_scene = need_scene || !same_spheres(g_cache[first + g]->scene, spheres, n);
+    if (need_scene) sd = &scene();
+    trace_mark("host_scene_ready");
+    if (!need_scene) {
+        // nothing to upload
+    } else if (G == 1) {
         work(0);
     } else {
         std::vector<std::thread> th;
         for (int g = 0; g < G; g++) th.emplace_back(work, g);
         for (auto& t : th) t.join();
-        trace_mark("contexts_on_device_threads");
+        trace_mark("scene_upload_on_device_threads");
     }
     for (int g = 0; g < G; g++)
         if (rcs[g]) {
@@ -1264,6 +1317,52 @@ int rt_render(const rt_camera* cam, const rt_sphere* spheres, size_t n, const rt
     }
     std::lock_guard<std::mutex> lock(g_cache_mu);  // also guards g_trace
     TraceScope trace;
+    // The host side of a new scene — device records, the SAH tree, and the tree trained on this
+    // camera's rays (≈11 ms for the final scene) — runs on a host thread while this one initialises
+    // the HIP runtime and the contexts (60-200 ms on a fresh process: the reference renders one
+    // image per process, main.zig:14-36).  Skipped when a cached context already holds the scene.
+    bool scene_cached = false;
+    for (rt_context* c : g_cache) scene_cached = scene_cached || (c && same_spheres(c->scene, spheres, n));
+    SceneData pre;
+    double prep_ms = 0;
+    std::thread prep;
+    bool pre_ready = false;
+    {
+        const uint32_t H0 = cam->image_height;
+        const int G0 = opts && opts->n_gpus > 0 ? std::min<int>(opts->n_gpus, (int)H0) : 1;  // rows of the first device
+        const uint64_t samples = (uint64_t)((H0 + (uint32_t)G0 - 1) / (uint32_t)G0) * cam->image_width * cam->samples_per_pixel;
+        auto job = [&pre, &prep_ms, spheres, n, cam, samples]() {
+            const auto t0 = std::chrono::steady_clock::now();
+            build_scene(spheres, n, pre);
+            prepare_tree(pre, *cam, samples);
+            prep_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        };
+        if (!scene_cached) {
+            try {
+                prep = std::thread(job);
+            } catch (const std::exception&) {  // no thread to be had: the scene is built inline below
+            }
+        }
+    }
+    // joins the host thread (or builds the scene inline) the first time the scene is needed
+    auto scene = [&]() -> const SceneData& {
+        if (!pre_ready) {
+            if (prep.joinable()) {
+                prep.join();
+                trace_note("host_scene_and_tree_thread", prep_ms);
+            } else {
+                build_scene(spheres, n, pre);
+            }
+            pre_ready = true;
+        }
+        return pre;
+    };
+    struct Joiner {  // every return path joins the host thread
+        std::thread& t;
+        ~Joiner() {
+            if (t.joinable()) t.join();
+        }
+    } joiner{prep};
     std::vector<int> map;
     rc = device_map(map);  // the process's first HIP call initialises the runtime
     if (rc) return rc;
@@ -1280,7 +1379,7 @@ int rt_render(const rt_camera* cam, const rt_sphere* spheres, size_t n, const rt
     const size_t px_bytes = o.output_format == RT_OUT_LINEAR_F64 ? 3 * sizeof(double) : 3;
 
     std::vector<rt_context*> ctxs;
-    rc = cached_contexts(map, first, G, spheres, n, ctxs);
+    rc = cached_contexts(map, first, G, spheres, n, scene, ctxs);
     if (rc) return rc;
     if (g_trace_on)
         for (rt_context* c : ctxs) (void)rt_context_enable_timing(c, 1);

@@ -26,11 +26,14 @@ ap.add_argument("--spp", type=int, default=100)
 ap.add_argument("--rounds", type=int, default=5)
 ap.add_argument("--env", default="RTZIG_KERNEL")
 ap.add_argument("--variants", default=os.environ.get("RTZIG_VARIANTS", "bvh smem_u4 lds_u4"))
+ap.add_argument("--row-step", type=int, default=1,
+                help="render rank 0's interleaved row set of an N-rank job (rows 0, N, 2N, ...)")
 args = ap.parse_args()
 
 cam = rtzig.final_scene_camera(width=args.width, aspect_ratio=args.aspect, spp=args.spp)
 H, W = cam.height, cam.width
-out = torch.empty((H, W, 3), dtype=torch.float64, device="cuda:0")
+R = (H + args.row_step - 1) // args.row_step
+out = torch.empty((R, W, 3), dtype=torch.float64, device="cuda:0")
 variants = args.variants.split()
 # one renderer per variant, with the variable set while the scene (and its BVH) is built too, so
 # the tool also A/Bs build-time knobs such as RTZIG_BVH_ALWAYS_AREA
@@ -47,9 +50,10 @@ for rnd in range(args.rounds + 1):
     for v in variants:
         os.environ[args.env] = v
         r = renderers[v]
-        r.render_rows_async(cam.cam, out.data_ptr())
+        r.render_rows_async(cam.cam, out.data_ptr(), row0=0, row_step=args.row_step, n_rows=R)
         torch.cuda.synchronize()
-        sm, _ = r.kernel_times()
+        sm, rm = r.kernel_times()
+        sm += rm  # direct mode's reduce pass belongs to the frame
         names[v] = r.kernel_name()
         img = out.cpu()
         if ref is None:
@@ -61,5 +65,6 @@ res = {}
 for v in variants:
     med = statistics.median(times[v])
     res[v] = {"kernel": names[v], "median_ms": round(med, 3), "min_ms": round(min(times[v]), 3),
-              "Msamples_s": round(W * H * args.spp / med / 1e3, 1)}
-print(json.dumps({"config": f"{W}x{H} {args.spp}spp", "env": args.env, "results": res}))
+              "Msamples_s": round(W * R * args.spp / med / 1e3, 1),
+              "workspace_bytes": renderers[v].workspace_bytes()}
+print(json.dumps({"config": f"{W}x{H} {args.spp}spp, rows 0::{args.row_step} ({R} rows)", "env": args.env, "results": res}))

@@ -107,6 +107,50 @@
 #define T_ADD_F32(X) "v_add_f32 " X ", " X ", %8\n"
 #define T_FMA_F32_SS(X) "v_fma_f32 " X ", " X ", %8, " X "\n"
 
+// Operand forms (round 5): the event-timed table showed v_fma_f32 at 2.2 cycles with two distinct
+// VGPR sources (x, b, x) and 4.2 with three (x, b, c), so an op's cost depends on its operands as
+// well as its opcode; %11 is a uniform 32-bit SGPR value.
+#define O_FMA_F32_S(X) "v_fma_f32 " X ", " X ", %11, %8\n"           /* 2 VGPR + SGPR */
+#define O_FMA_F32_K(X) "v_fma_f32 " X ", " X ", 0.5, %8\n"           /* 2 VGPR + inline constant */
+#define O_PK_FMA_2(X) "v_pk_fma_f32 " X ", " X ", %8, " X "\n"       /* 2 distinct VGPR pairs */
+#define O_PK_FMA_LO(X) "v_pk_fma_f32 " X ", " X ", %8, %9 op_sel_hi:[1,0,0]\n" /* broadcast lo halves */
+#define O_PK_ADD_2(X) "v_pk_add_f32 " X ", " X ", " X "\n"
+#define O_PK_MUL_S(X) "v_pk_mul_f32 " X ", " X ", %10\n"
+#define O_ADD_F64_S(X) "v_add_f64 " X ", " X ", %10\n"
+#define O_ADD_F64_K(X) "v_add_f64 " X ", " X ", 1.0\n"
+#define O_FMA_F64_2(X) "v_fma_f64 " X ", " X ", %8, " X "\n"
+#define O_MUL_F64_SELF(X) "v_mul_f64 " X ", " X ", " X "\n"
+#define O_MAX_F32_K(X) "v_max_f32 " X ", 0.5, " X "\n"
+#define O_MAX_F32_S(X) "v_max_f32 " X ", %11, " X "\n"
+#define O_MIN3_F32_2(X) "v_min3_f32 " X ", " X ", %8, " X "\n"
+#define O_MIN3_F32_S(X) "v_min3_f32 " X ", " X ", %8, %11\n"
+#define O_LSHL_S(X) "v_lshlrev_b32 " X ", %11, " X "\n"
+#define O_LSHL_V(X) "v_lshlrev_b32 " X ", %8, " X "\n"
+#define O_LSHR_V(X) "v_lshrrev_b32 " X ", %8, " X "\n"
+#define O_OR(X) "v_or_b32 " X ", " X ", %8\n"
+#define O_OR3(X) "v_or3_b32 " X ", " X ", %8, %9\n"
+#define O_ADD3_2(X) "v_add3_u32 " X ", " X ", %8, " X "\n"
+#define O_ADD3_S(X) "v_add3_u32 " X ", " X ", %8, %11\n"
+#define O_BITOP3_2(X) "v_bitop3_b32 " X ", " X ", %8, " X " bitop3:0x96\n"
+#define O_BITOP3_S(X) "v_bitop3_b32 " X ", " X ", %8, %11 bitop3:0x96\n"
+#define O_XOR_S(X) "v_xor_b32 " X ", %11, " X "\n"
+#define O_ADD_U32_K(X) "v_add_u32 " X ", 0x1234, " X "\n"
+#define O_CNDMASK_K(X) "v_cndmask_b32_e64 " X ", " X ", 0, %10\n"
+#define O_MUL_U24(X) "v_mul_u32_u24 " X ", " X ", %8\n"
+#define O_MAD_U24(X) "v_mad_u32_u24 " X ", " X ", %8, %9\n"
+#define O_CVT_F32_U32(X) "v_cvt_f32_u32 " X ", %8\n"
+#define O_ALIGNBIT_S(X) "v_alignbit_b32 " X ", " X ", %11, 9\n"
+#define O_LSHL_ADD_2(X) "v_lshl_add_u32 " X ", " X ", 2, " X "\n"
+#define O_ADD_LSHL(X) "v_add_lshl_u32 " X ", " X ", %8, 2\n"
+#define O_PERM(X) "v_perm_b32 " X ", " X ", %8, %9\n"
+#define O_MOV_DPP(X) "v_mov_b32_dpp " X ", %8 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n"
+#define O_SUBREV(X) "v_subrev_u32 " X ", %8, " X "\n"
+#define O_MUL_F32_K(X) "v_mul_f32 " X ", 0.5, " X "\n"
+#define O_FMAC_F32(X) "v_fmac_f32 " X ", %8, %9\n"                 /* dst is the accumulator */
+#define O_FMAC_F64(X) "v_fmac_f64 " X ", %8, %9\n"
+#define O_PK_MOV(X) "v_pk_mov_b32 " X ", %8, %9 op_sel:[0,1]\n"
+#define O_LSHL_ADD_U64_2(X) "v_lshl_add_u64 " X ", " X ", 0, " X "\n"
+
 struct Stamp {
     unsigned long long t0, t1, r0, r1;  // s_memtime, s_memrealtime at loop start / end
 };
@@ -121,11 +165,12 @@ __device__ __forceinline__ double fold(T x) { return (double)x; }
           a4 = INIT(lane, 4), a5 = INIT(lane, 5), a6 = INIT(lane, 6), a7 = INIT(lane, 7);               \
         const BT b = BINIT(lane), c = CINIT(lane);                                                      \
         const uint64_t m = __builtin_amdgcn_read_exec() ^ (uint64_t)(blockIdx.x & 1u);                  \
+        const uint32_t su = 0x3f800001u + (blockIdx.x & 7u); /* a uniform 32-bit value (f32 ~1.0) */    \
         const unsigned long long t0 = __builtin_amdgcn_s_memtime();                                     \
         const unsigned long long r0 = __builtin_amdgcn_s_memrealtime();                                 \
         for (int i = 0; i < iters; ++i)                                                                 \
             asm volatile(IND8(INS) : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5),        \
-                         "+v"(a6), "+v"(a7) : "v"(b), "v"(c), "s"(m) : "vcc");                          \
+                         "+v"(a6), "+v"(a7) : "v"(b), "v"(c), "s"(m), "s"(su) : "vcc");                 \
         const unsigned long long t1 = __builtin_amdgcn_s_memtime();                                     \
         const unsigned long long r1 = __builtin_amdgcn_s_memrealtime();                                 \
         if (threadIdx.x == 0) st[blockIdx.x] = Stamp{t0, t1, r0, r1};                                   \
@@ -183,6 +228,16 @@ KL(cmp_u64, T_CMP_U64) KU(lshr_b32, T_LSHR_B32) KU(and32, T_AND_B32) KL(lshl_b64
 KU(sub_u32, T_SUB_U32) KU(max_i32, T_MAX_I32) KU(min_i32, T_MIN_I32) KU(max3_i32, T_MAX3_I32) KU(min3_i32, T_MIN3_I32)
 KU(max_u32, T_MAX_U32) KU(cmp_le_i32, T_CMP_LE_I32) KF(maximum3_f32, T_MAXIMUM3_F32) KF(min_f32, T_MIN_F32)
 KF(sub_f32, T_SUB_F32) KP(pk_add_f32, T_PK_ADD_F32) KP(pk_mul_f32, T_PK_MUL_F32) KU(ashr_i32, T_ASHR_I32)
+KF(o_fma_f32_s, O_FMA_F32_S) KF(o_fma_f32_k, O_FMA_F32_K) KP(o_pk_fma_2, O_PK_FMA_2) KP(o_pk_fma_lo, O_PK_FMA_LO)
+KP(o_pk_add_2, O_PK_ADD_2) KP(o_pk_mul_s, O_PK_MUL_S) KD(o_add_f64_s, O_ADD_F64_S) KD(o_add_f64_k, O_ADD_F64_K)
+KD(o_fma_f64_2, O_FMA_F64_2) KD(o_mul_f64_self, O_MUL_F64_SELF) KF(o_max_f32_k, O_MAX_F32_K) KF(o_max_f32_s, O_MAX_F32_S)
+KF(o_min3_f32_2, O_MIN3_F32_2) KF(o_min3_f32_s, O_MIN3_F32_S) KU(o_lshl_s, O_LSHL_S) KU(o_lshl_v, O_LSHL_V)
+KU(o_lshr_v, O_LSHR_V) KU(o_or, O_OR) KU(o_or3, O_OR3) KU(o_add3_2, O_ADD3_2) KU(o_add3_s, O_ADD3_S)
+KU(o_bitop3_2, O_BITOP3_2) KU(o_bitop3_s, O_BITOP3_S) KU(o_xor_s, O_XOR_S) KU(o_add_u32_k, O_ADD_U32_K)
+KU(o_cndmask_k, O_CNDMASK_K) KU(o_mul_u24, O_MUL_U24) KU(o_mad_u24, O_MAD_U24) KU(o_cvt_f32_u32, O_CVT_F32_U32)
+KU(o_alignbit_s, O_ALIGNBIT_S) KU(o_lshl_add_2, O_LSHL_ADD_2) KU(o_add_lshl, O_ADD_LSHL) KU(o_perm, O_PERM)
+KU(o_mov_dpp, O_MOV_DPP) KU(o_subrev, O_SUBREV) KF(o_mul_f32_k, O_MUL_F32_K) KF(o_fmac_f32, O_FMAC_F32)
+KD(o_fmac_f64, O_FMAC_F64) KP(o_pk_mov, O_PK_MOV) KL(o_lshl_add_u64_2, O_LSHL_ADD_U64_2)
 KU(alignbit_same, T_ALIGNBIT_SAME) KERNEL(cvt_f32_f64_in, float, double, T_CVT_F32_F64, F32_INIT, F64_B_MUL, F64_C) KF(add_f32, T_ADD_F32) KF(fma_f32_ss, T_FMA_F32_SS)
 
 struct Op {
@@ -229,6 +284,26 @@ int main(int argc, char** argv) {
         {"v_ashrrev_i32", k_ashr_i32, 1, "Tops/s"}, {"v_alignbit_b32 (x, x: rotate)", k_alignbit_same, 1, "Tops/s"},
         {"v_cvt_f32_f64", k_cvt_f32_f64_in, 1, "Tops/s"}, {"v_add_f32", k_add_f32, 1, "TFLOP/s"},
         {"v_fma_f32 (x, b, x)", k_fma_f32_ss, 2, "TFLOP/s"},
+        {"v_fma_f32 (x, s, b)", k_o_fma_f32_s, 2, "TFLOP/s"}, {"v_fma_f32 (x, 0.5, b)", k_o_fma_f32_k, 2, "TFLOP/s"},
+        {"v_pk_fma_f32 (x, b, x)", k_o_pk_fma_2, 4, "TFLOP/s"}, {"v_pk_fma_f32 (x, b, c) op_sel_hi:[1,0,0]", k_o_pk_fma_lo, 4, "TFLOP/s"},
+        {"v_pk_add_f32 (x, x)", k_o_pk_add_2, 2, "TFLOP/s"}, {"v_pk_mul_f32 (x, s)", k_o_pk_mul_s, 2, "TFLOP/s"},
+        {"v_add_f64 (x, s)", k_o_add_f64_s, 1, "TFLOP/s"}, {"v_add_f64 (x, 1.0)", k_o_add_f64_k, 1, "TFLOP/s"},
+        {"v_fma_f64 (x, b, x)", k_o_fma_f64_2, 2, "TFLOP/s"}, {"v_mul_f64 (x, x)", k_o_mul_f64_self, 1, "TFLOP/s"},
+        {"v_max_f32 (0.5, x)", k_o_max_f32_k, 1, "Tops/s"}, {"v_max_f32 (s, x)", k_o_max_f32_s, 1, "Tops/s"},
+        {"v_min3_f32 (x, b, x)", k_o_min3_f32_2, 1, "Tops/s"}, {"v_min3_f32 (x, b, s)", k_o_min3_f32_s, 1, "Tops/s"},
+        {"v_lshlrev_b32 (s, x)", k_o_lshl_s, 1, "Tops/s"}, {"v_lshlrev_b32 (b, x)", k_o_lshl_v, 1, "Tops/s"},
+        {"v_lshrrev_b32 (b, x)", k_o_lshr_v, 1, "Tops/s"}, {"v_or_b32", k_o_or, 1, "Tops/s"},
+        {"v_or3_b32", k_o_or3, 1, "Tops/s"}, {"v_add3_u32 (x, b, x)", k_o_add3_2, 1, "Tops/s"},
+        {"v_add3_u32 (x, b, s)", k_o_add3_s, 1, "Tops/s"}, {"v_bitop3_b32 (x, b, x)", k_o_bitop3_2, 1, "Tops/s"},
+        {"v_bitop3_b32 (x, b, s)", k_o_bitop3_s, 1, "Tops/s"}, {"v_xor_b32 (s, x)", k_o_xor_s, 1, "Tops/s"},
+        {"v_add_u32 (0x1234, x)", k_o_add_u32_k, 1, "Tops/s"}, {"v_cndmask_b32_e64 (x, 0, s)", k_o_cndmask_k, 1, "Tops/s"},
+        {"v_mul_u32_u24", k_o_mul_u24, 1, "Tops/s"}, {"v_mad_u32_u24", k_o_mad_u24, 1, "Tops/s"},
+        {"v_cvt_f32_u32", k_o_cvt_f32_u32, 1, "Tops/s"}, {"v_alignbit_b32 (x, s)", k_o_alignbit_s, 1, "Tops/s"},
+        {"v_lshl_add_u32 (x, 2, x)", k_o_lshl_add_2, 1, "Tops/s"}, {"v_add_lshl_u32", k_o_add_lshl, 1, "Tops/s"},
+        {"v_perm_b32", k_o_perm, 1, "Tops/s"}, {"v_mov_b32_dpp", k_o_mov_dpp, 1, "Tops/s"},
+        {"v_subrev_u32", k_o_subrev, 1, "Tops/s"}, {"v_mul_f32 (0.5, x)", k_o_mul_f32_k, 1, "TFLOP/s"},
+        {"v_fmac_f32 (b, c)", k_o_fmac_f32, 2, "TFLOP/s"}, {"v_fmac_f64 (b, c)", k_o_fmac_f64, 2, "TFLOP/s"},
+        {"v_pk_mov_b32", k_o_pk_mov, 1, "Tops/s"}, {"v_lshl_add_u64 (x, 0, x)", k_o_lshl_add_u64_2, 1, "Tops/s"},
     };
     const bool want_table = argc > 2 && std::atoi(argv[2]) != 0;
     int cus = 0, dev_clock_khz = 0;
@@ -282,8 +357,10 @@ int main(int argc, char** argv) {
                 cus, simds, dev_clock_khz / 1000.0, target_ms);
     bool first = true;
     std::vector<std::pair<const Op*, int>> plan;
-    for (const Op& op : ops)
-        for (int wps : {1, 2, 4, 8}) plan.push_back({&op, wps});
+    const bool table_only = argc > 2 && std::atoi(argv[2]) == 2;
+    if (!table_only)
+        for (const Op& op : ops)
+            for (int wps : {1, 2, 4, 8}) plan.push_back({&op, wps});
     if (want_table)
         for (const Op& op : table)
             for (int wps : {4, 8}) plan.push_back({&op, wps});

@@ -11,18 +11,18 @@ launches (sample chunks); every counter is summed over the timed kernel's dispat
 Units (MI355X_MICROARCH.md): FETCH_SIZE / WRITE_SIZE in KiB; SQ_WAVE_CYCLES, SQ_WAIT_*,
 SQ_ACTIVE_INST_* and SQ_BUSY_CYCLES count quad-cycles; SQ_INSTS_* count wave-instructions; the
 effective clock is GRBM_GUI_ACTIVE / 8 XCDs / the kernel's wall time.
-VALU issue model, MEASURED on the MI355X (round 4, tools/valu_rates.hip,
-profiles/r04_valu_rates/): SIMD cycles per wave64 instruction at the kernel's 4 waves per SIMD.
-f64 add/mul/fma issue at 2.12 (full rate on CDNA4, not half), rsq/rcp_f64 at 7.94, rcp_f32 at 6.03;
-the other 32/64-bit ops split into a 2.0 class (add, xor, and, mov, bitop3, 64-bit shifts, f64
-compares) and a 3.0-3.1 class (32-bit min/max/compare/cndmask, alignbit, mul_lo, mad_u64_u32, bfi).
-The mix of the latter comes from the kernel's own instruction stream: profiles/<tag>/region_table.json
-(tools/region_table.py) prices every opcode of the shipped kernel with its measured rate, weighted by
-the exact per-region executions of one instrumented frame; its mean cycles per VALU instruction of the
-non-f64, non-transcendental ops prices the PMC's "other" count:
-    issue cycles = 2.12 n_f64 + 7.94 n_trans_f64 + 6.03 n_trans_f32 + r_other n_other,
+VALU issue model, MEASURED on the MI355X with event timing (round 5, tools/peak_rates.hip ->
+profiles/r05_peak/issue_rates.json, tools/issue_rates.py): SIMD cycles per wave64 instruction.
+f64 add/mul/fma 4.17 (16 lanes per clock: the 78.6 TF/s spec), rsq/rcp_f64 16.1, f32 transcendentals
+8.1; the other ops cost 4.15, or 2.2 for the fast 32-bit forms (add/sub/and/or/xor/mov/lshr, f32
+add/mul/fma, bitop3) with at most two distinct VGPR sources and no SGPR.  The mean of the "other"
+class comes from the kernel's own instruction stream: profiles/<tag>/region_table.json
+(tools/region_table.py) prices every instruction of the shipped kernel, operands included, weighted
+by the exact per-region executions of one instrumented frame:
+    issue cycles = 4.17 n_f64 + 16.1 n_trans_f64 + 8.1 n_trans_f32 + r_other n_other,
     frac = issue / (1024 SIMDs x clock x t)
-(rounds 1-3 used the guide's nominal 2 / 4 / 8 cycles, which overprices f64 by 2x.)
+(round 4's s_memtime table, 2.12 / 7.94 / 6.03 / 2.49, assumed co-resident waves that were not:
+profiles/r05_peak/README.md.)
 """
 import csv
 import glob
@@ -95,17 +95,17 @@ def main(tag, workload):
             n64 = g("SQ_INSTS_VALU_ADD_F64") + g("SQ_INSTS_VALU_MUL_F64") + g("SQ_INSTS_VALU_FMA_F64")
             ntr64, ntr32 = g("SQ_INSTS_VALU_TRANS_F64"), g("SQ_INSTS_VALU_TRANS_F32")
             n32 = g("SQ_INSTS_VALU") - n64 - ntr64 - ntr32
-            r_other, src_other = 2.6, "assumed (no region table for this tag)"
+            r_other, src_other = 3.84, "assumed (round 4's kernel, profiles/r05_peak/README.md)"
             rtab = os.path.join(dst, "region_table.json")
             if os.path.exists(rtab):
                 r_other = json.load(open(rtab))["total_est"]["other_valu_cycles_per_instruction"]
                 src_other = f"profiles/{tag}/region_table.json"
-            cyc = 2.12 * n64 + 7.94 * ntr64 + 6.03 * ntr32 + r_other * n32
+            cyc = 4.17 * n64 + 16.1 * ntr64 + 8.1 * ntr32 + r_other * n32
             out["valu_issue_cycles_per_frame"] = cyc
             out["valu_issue_frac_pmc_pass"] = cyc / (SIMDS * clock * T)
-            out["valu_issue_model"] = {"f64_add_mul_fma": 2.12, "trans_f64": 7.94, "trans_f32": 6.03,
+            out["valu_issue_model"] = {"f64_add_mul_fma": 4.17, "trans_f64": 16.1, "trans_f32": 8.1,
                                        "other": round(r_other, 4), "other_source": src_other,
-                                       "rates": "profiles/r04_valu_rates/valu_rates_b.json"}
+                                       "rates": "profiles/r05_peak/issue_rates.json (event-timed)"}
             out["valu_issue_cycles_nominal_guide_model"] = 2 * n32 + 4 * n64 + 8 * (ntr64 + ntr32)
             out["valu_insts"] = {"total": g("SQ_INSTS_VALU"), "f64": n64, "trans": ntr64 + ntr32, "other_32bit": n32}
         if "SQ_WAVE_CYCLES" in sums and "SQ_ACTIVE_INST_ANY" in sums:

@@ -20,11 +20,13 @@
    Every block of a region is assumed to run whenever the region runs (a wave executes each branch
    some lane takes), so the estimate is an upper bound per region; the sum is compared with the
    PMC count of VALU instructions.
-4. Prices every VALU opcode with its MEASURED issue cost on the MI355X (tools/valu_rates.hip,
-   profiles/r04_valu_rates/valu_rates_b.json: SIMD cycles per wave64 instruction with 4 waves per
-   SIMD, the kernel's occupancy): e.g. f64 add/mul/fma/max/compare, 32-bit add/xor/and/mov, bitop3,
-   pk_fma 1.9-2.1; 32-bit min/max/compare/cndmask, alignbit, mul_lo, mad_u64_u32, bfi, lshlrev_b32
-   3.0-3.1; rcp_f32 6.0; rsq/rcp_f64 7.9.  An opcode the table lacks takes its class's rate.
+4. Prices every VALU instruction with its MEASURED issue cost on the MI355X (round 5:
+   tools/peak_rates.hip, event-timed over every CU, profiles/r05_peak/issue_rates.json via
+   tools/issue_rates.py): ~4.15 SIMD cycles per wave64 instruction for f64, 64-bit integer, packed
+   f32, min/max, compare, cndmask, alignbit, mul, mad, bfi ops; ~2.2 for the "fast" 32-bit ops
+   (add/sub/and/or/xor/not/mov/lshr/ashr, f32 add/sub/mul/fma, bitop3) when they read at most two
+   distinct VGPRs and no SGPR, 4.15 otherwise; 8.1 for v_rcp_f32; 16.1 for v_rsq/rcp_f64.  (Round 4's
+   s_memtime table, profiles/r04_valu_rates/, was off by 1.4-2x: its waves were not all co-resident.)
 
     python tools/region_table.py <kprof.json> [--spp-scale 5] [--pmc profiles/r04/summary.json] [--out F]
 """
@@ -42,7 +44,10 @@ KERNEL = "_ZN3rtk17sample_kernel_bvhILb1ELb0ELb0E"
 F64 = re.compile(r"^v_(add|mul|fma|fmac)_f64|^v_(rsq|rcp|sqrt)_f64|^v_div_(scale|fmas|fixup)_f64|^v_cmp\w*_f64|^v_(min|max)_f64|^v_cvt_f64")
 
 
-RATES = os.path.join(ROOT, "profiles", "r04_valu_rates", "valu_rates_b.json")
+RATES = os.path.join(ROOT, "profiles", "r05_peak", "issue_rates.json")
+import sys  # noqa: E402
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import issue_rates  # noqa: E402
 
 
 def load_rates(path=RATES):
@@ -180,6 +185,7 @@ def main():
     ap.add_argument("kprof")
     ap.add_argument("--spp-scale", type=float, default=5.0, help="frame spp / kprof spp (500 / 100)")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r04", "summary.json"))
+    ap.add_argument("--asm", default=None, help="price this assembly file instead of compiling (RTZIG_MARKS build)")
     ap.add_argument("--out", default=None)
     ap.add_argument("-D", action="append", default=[], help="extra -D for the build (variants)")
     args = ap.parse_args()
@@ -187,7 +193,8 @@ def main():
     sc = args.spp_scale
     n = {"iter": raw[26] * sc, "trips": raw[27] * sc, "seed": raw[28] * sc, "wstart": raw[29] * sc, "shade": raw[30] * sc,
          "inner": raw[7] * sc, "leaf": raw[8] * sc, "cand": raw[9] * sc, "root2": raw[10] * sc, "fin": raw[31] * sc}
-    blocks = blocks_of(asm(["-DRTZIG_MARKS=1"] + ["-D" + d for d in args.D]), KERNEL)
+    lines = open(args.asm).read().split("\n") if args.asm else asm(["-DRTZIG_MARKS=1"] + ["-D" + d for d in args.D])
+    blocks = blocks_of(lines, KERNEL)
     per, succ = regions(blocks)
     static = collections.defaultdict(lambda: collections.Counter())
     inner_loop = {k for k, ss in succ.items() if k in ss and any(klass(i) == "lds" for i in blocks[k]["ins"])
@@ -206,10 +213,12 @@ def main():
         return seen
     ws_loop = {k for k in ws_blocks if k in reach(k)}
     dyn = collections.defaultdict(lambda: collections.Counter())
-    rates = load_rates()
+    table = issue_rates.load(RATES)
     cyc = collections.Counter()    # measured-rate VALU issue cycles per region
     other = collections.Counter()  # the ops outside the PMC's f64 add/mul/fma and transcendental classes
     opcyc = collections.Counter()  # ... per opcode (whole kernel)
+    opcnt = collections.Counter()  # executions per opcode
+    regop = collections.Counter()  # issue cycles per (region, opcode)
     unpriced = collections.Counter()
     for k, r, ins in per:
         c = klass(ins)
@@ -239,12 +248,14 @@ def main():
         dyn[r][c] += w
         op = ins.split()[0]
         if op.startswith("v_"):
-            rt = rate(op, rates)
+            rt = issue_rates.price(ins, table)
             base = re.sub(r"_(e32|e64|sdwa|dpp)$", "", op)
-            if base not in rates:
+            if base not in table["opcodes"] and base not in table["fast_rule"]["opcodes"]:
                 unpriced[op] += w
             cyc[r] += w * rt
             opcyc[op] += w * rt
+            opcnt[op] += w
+            regop[(r, op)] += w * rt
             if r not in ("rare", "prologue", "epilogue", "?") and not re.match(
                     r"^v_(add|mul|fma|fmac)_f64|^v_(rsq|rcp|sqrt|exp|log|sin|cos)_f(32|64)", op):
                 other["n"] += w
@@ -272,9 +283,12 @@ def main():
                          "valu_cycles_per_instruction": tcyc / tval if tval else None,
                          "other_valu_cycles_per_instruction": other["cyc"] / other["n"] if other["n"] else None},
            "rates": {"source": os.path.relpath(RATES, ROOT),
-                     "model": "SIMD cycles per wave64 instruction at 4 waves/SIMD, measured per opcode"},
-           "top_opcodes_by_issue_cycles": [{"op": o, "cycles": c, "share": round(c / tcyc, 4), "rate": rate(o, rates)}
+                     "model": "SIMD cycles per wave64 instruction, event-timed per opcode and operand form (round 5)"},
+           "top_opcodes_by_issue_cycles": [{"op": o, "cycles": c, "share": round(c / tcyc, 4),
+                                            "mean_rate": round(c / opcnt[o], 3)}
                                            for o, c in opcyc.most_common(25)],
+           "top_region_opcodes": [{"region": k[0], "op": k[1], "share": round(c / tcyc, 4)}
+                                  for k, c in regop.most_common(40)],
            "unpriced_opcodes (sibling rate used)": {o: c for o, c in unpriced.most_common(10)}}
     try:
         pm = json.load(open(args.pmc))["counters_per_frame"]
