@@ -354,7 +354,7 @@ def run(args):
         if w == 0:
             first_ms = (time.perf_counter() - t_w) * 1e3
     # one untimed instrumented frame: exact executed-work counts (sphere tests, BVH node visits)
-    pstats = torch.zeros(32, dtype=torch.int64, device=dev)
+    pstats = torch.zeros(rtzig.abi.RT_PROFILE_STATS_WORDS, dtype=torch.int64, device=dev)
     if n_rows:
         renderer.enable_profile(True)
         renderer.render_rows_async(cam.cam, out.data_ptr(), row0=row0, row_step=step, n_rows=n_rows,

@@ -624,7 +624,7 @@ def test_direct_rows_instrumented_bit_exact(oracle, profile, monkeypatch):
     r.set_scene(cam.scene.world)
     r.enable_profile(profile)
     out = torch.zeros((12, 1200, 3), dtype=torch.float64, device="cuda:0")
-    stats = torch.zeros(32, dtype=torch.int64, device="cuda:0")
+    stats = torch.zeros(rtzig.abi.RT_PROFILE_STATS_WORDS, dtype=torch.int64, device="cuda:0")
     r.render_rows_async(cam.cam, out.data_ptr(), row0=3, row_step=8, n_rows=12, d_stats_ptr=stats.data_ptr())
     r.sync()
     assert "direct" in r.kernel_name() and ("prof" in r.kernel_name()) == profile

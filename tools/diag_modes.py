@@ -79,7 +79,7 @@ for li, path in enumerate(args.libs):
         L.rt_context_set_precision(ctx, prec)
         L.rt_context_enable_profile(ctx, int(prof))
         out = torch.zeros((n, cam.width, 3), dtype=torch.float64, device="cuda:0")
-        stats = torch.zeros(32, dtype=torch.int64, device="cuda:0")
+        stats = torch.zeros(rtzig.abi.RT_PROFILE_STATS_WORDS, dtype=torch.int64, device="cuda:0")
         rec = {"lib": path, "case": name}
         rc = L.rt_render_rows_async(ctx, C.byref(cam.cam), 0, row0, step, n, C.c_void_p(out.data_ptr()),
                                     C.c_void_p(stats.data_ptr()), None)

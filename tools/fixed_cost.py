@@ -19,7 +19,7 @@ for bm in (50, 2):
         r.set_scene(cam.scene.world)
         r.enable_timing(True)
         out = torch.empty((100, W, 3), dtype=torch.float64, device="cuda:0")
-        st = torch.zeros(32, dtype=torch.int64, device="cuda:0")
+        st = torch.zeros(rtzig.abi.RT_PROFILE_STATS_WORDS, dtype=torch.int64, device="cuda:0")
         ks, rs = [], []
         for _ in range(5):
             r.render_rows_async(cam.cam, out.data_ptr(), row0=0, row_step=8, n_rows=100)

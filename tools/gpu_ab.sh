@@ -1,16 +1,10 @@
 #!/bin/bash
-# GPU round trip for a kernel change: pytest -m gpu (parity) -> in-process A/B of ab/*.so builds.
-#   AB="ab/base.so ab/new.so" SPP=100 tools/gpu_ab.sh
-# Every GPU step has its own time limit; the script stops at the first failing step.
+# In-process A/B of the libraries in $AB: config 4's frame at 100 spp and rank 0's rows of an
+# 8-GPU job at 500 spp (tools/ab_libs.py), nothing else.
 cd "$GRAFT_REPO_ROOT" || exit 2
 mkdir -p gpurun_out
-AB=${AB:-"ab/base.so ab/new.so"}
-SPP=${SPP:-100}
-if [ -z "$SKIP_TESTS" ]; then
-  timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
-  rc=$?; echo "pytest rc=$rc"; tail -15 gpurun_out/pytest_gpu.log
-  [ $rc -eq 0 ] || exit $rc
-fi
-timeout -k 10 300 python -u tools/ab_libs.py $AB --spp $SPP --rounds ${ROUNDS:-5} > gpurun_out/ab.json 2> gpurun_out/ab.err
-rc=$?; echo "ab rc=$rc"; cat gpurun_out/ab.json; tail -5 gpurun_out/ab.err
-exit $rc
+T=${TAG:-ab}
+timeout -k 10 300 python3 -u tools/ab_libs.py $AB --spp 100 --rounds 7 > gpurun_out/ab_$T.json 2> gpurun_out/ab_$T.err
+rc=$?; echo "ab rc=$rc"; cat gpurun_out/ab_$T.json; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python3 -u tools/ab_libs.py $AB --spp 500 --rounds 7 --row-step 8 > gpurun_out/ab_${T}_r8.json 2> gpurun_out/ab_${T}_r8.err
+rc=$?; echo "ab8 rc=$rc"; cat gpurun_out/ab_${T}_r8.json; exit $rc

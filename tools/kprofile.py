@@ -39,7 +39,7 @@ r.enable_timing(True)
 row0, step, n_rows = (0, 1, H) if args.rows is None else tuple(int(x) for x in args.rows.split(":"))
 rows = dict(row0=row0, row_step=step, n_rows=n_rows)
 out = torch.empty((n_rows, W, 3), dtype=torch.float64, device="cuda:0")
-stats = torch.zeros(32, dtype=torch.int64, device="cuda:0")
+stats = torch.zeros(rtzig.abi.RT_PROFILE_STATS_WORDS, dtype=torch.int64, device="cuda:0")
 res = {"config": f"{W}x{H} {args.spp}spp, {len(cam.scene.world)} spheres", "variants": {}}
 for v in args.variants.split():
     os.environ["RTZIG_KERNEL"] = v

@@ -77,9 +77,10 @@ def pipeline_ms(row0, step, n_rows):
 
     def frame(k):
         b, pb = k % 2, (k - 1) % 2
-        wb = pb if pend[0] else b  # the row buffer this frame's kernel writes (deferred fold, or its own rows)
-        if freed[wb] is not None:
-            render.wait_event(freed[wb])
+        # the kernel writes its own rows (outs[b]) and, with a pass pending, folds into outs[pb]
+        for wb in ((b, pb) if pend[0] else (b,)):
+            if freed[wb] is not None:
+                render.wait_event(freed[wb])
         r.render_rows_async(cam.cam, outs[b].data_ptr(), row0=row0, row_step=step, n_rows=n_rows,
                             stream_ptr=render.cuda_stream, out_stream_ptr=coll.cuda_stream, deferred=deferred)
         if pend[0]:
@@ -109,15 +110,19 @@ def pipeline_ms(row0, step, n_rows):
         torch.cuda.synchronize()
         ms = (time.perf_counter() - t0) / args.pipe_frames * 1e3
         best = ms if best is None else min(best, ms)
+    ws[0] = max(ws[0], r.workspace_bytes())
     return best
 
 
-res = {"config": f"{W}x{H} {args.spp}spp", "link_GBps_model": LINK_GBPS, "launch_us_model": LAUNCH_US, "ranks": {}}
+ws = [0]  # the largest workspace a rank's pipeline held (rt_context_workspace_bytes)
+res = {"config": f"{W}x{H} {args.spp}spp", "unit_mode_env": os.environ.get("RTZIG_UNIT_MODE"),
+       "pipe_mode": args.pipe_mode if args.pipe_frames else None, "link_GBps_model": LINK_GBPS, "launch_us_model": LAUNCH_US, "ranks": {}}
 base = None
 pipe_base = None
 for n in args.ns:
     R = rdist.rows_per_rank(H, n)
     per_rank, per_rank_pipe = [], []
+    ws[0] = 0
     for rank in range(n):
         row0, step, n_rows = rdist.rank_rows(H, rank, n)
         per_rank.append(kernel_ms(row0, step, n_rows))
@@ -157,5 +162,6 @@ for n in args.ns:
         pipe_base = pipe_base or pf
         res["ranks"][n].update({"pipelined_frame_ms_max_over_ranks": round(max(per_rank_pipe), 3),
                                 "pipelined_frame_ms_min_over_ranks": round(min(per_rank_pipe), 3),
-                                "efficiency_pipelined": round(pipe_base / pf / n, 3)})
+                                "efficiency_pipelined": round(pipe_base / pf / n, 3),
+                                "workspace_GiB_max_over_ranks": round(ws[0] / 2**30, 3)})
 print(json.dumps(res))

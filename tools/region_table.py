@@ -192,7 +192,10 @@ def main():
     raw = json.load(open(args.kprof))["variants"]["bvh"]["raw"]
     sc = args.spp_scale
     n = {"iter": raw[26] * sc, "trips": raw[27] * sc, "seed": raw[28] * sc, "wstart": raw[29] * sc, "shade": raw[30] * sc,
-         "inner": raw[7] * sc, "leaf": raw[8] * sc, "cand": raw[9] * sc, "root2": raw[10] * sc, "fin": raw[31] * sc}
+         "inner": raw[7] * sc, "leaf": raw[8] * sc, "cand": raw[9] * sc, "root2": raw[10] * sc, "fin": raw[31] * sc,
+         # seed-window passes (round 5; older profiles have 32 words: estimated as one per 64 samples)
+         "win": (raw[32] - raw[33] if len(raw) > 33 and raw[32] else raw[1] / 64) * sc,
+         "win2": (raw[33] if len(raw) > 33 and raw[32] else raw[1] / 64 / 50) * sc}
     lines = open(args.asm).read().split("\n") if args.asm else asm(["-DRTZIG_MARKS=1"] + ["-D" + d for d in args.D])
     blocks = blocks_of(lines, KERNEL)
     per, succ = regions(blocks)
@@ -238,6 +241,10 @@ def main():
             w = n["trips"] / 3
         elif r == "seed":
             w = n["seed"]
+        elif r == "seed_window":
+            w = n["win"]
+        elif r == "seed_window2":
+            w = n["win2"]
         elif r == "shade":
             w = n["shade"]
         elif r == "fin_work":
@@ -260,7 +267,7 @@ def main():
                     r"^v_(add|mul|fma|fmac)_f64|^v_(rsq|rcp|sqrt|exp|log|sin|cos)_f(32|64)", op):
                 other["n"] += w
                 other["cyc"] += w * rt
-    order = ["finalise", "fin_work", "handout", "seed", "idle", "trips", "scatter_finish", "walk_setup", "walk_inner", "leaf", "shade",
+    order = ["finalise", "fin_work", "handout", "seed", "seed_window", "seed_window2", "idle", "trips", "scatter_finish", "walk_setup", "walk_inner", "leaf", "shade",
              "store", "rare", "prologue", "epilogue", "?"]
     rows = []
     tot = collections.Counter()
