@@ -150,8 +150,10 @@ def parse_args(argv=None):
                     help="at --gpus 1, still join a (1-rank) process group on --dist-backend and run the "
                          "N>1 pipeline: two row buffers, the render stream, and each frame's dist.gather on "
                          "the collective stream (nccl: the RCCL gather on one GPU)")
-    ap.add_argument("--pipeline", choices=["split", "deferred"], default="deferred",
-                    help="N > 1 frame loop: 'split' completes each frame's output on the collective stream "
+    ap.add_argument("--pipeline", choices=["plain", "split", "deferred"], default="deferred",
+                    help="N > 1 frame loop: 'plain' completes each frame on the render stream (one "
+                         "per-sample buffer in direct mode: half the workspace, the reduce pass on the "
+                         "critical path); 'split' completes each frame's output on the collective stream "
                          "(rt_render_rows_async_split); 'deferred' also leaves a direct-mode frame's reduce "
                          "pass to the next frame's drained waves (rt_render_rows_async_deferred), gathering "
                          "each frame once the next one is issued")
@@ -327,7 +329,14 @@ def run(args):
                                            n_rows=n_rows, output=args.output, d_stats_ptr=stats_ptr,
                                            stream_ptr=stream.cuda_stream)
             return gather(buf)
-        if n_rows:
+        if n_rows and args.pipeline == "plain":
+            # one per-sample buffer: sample kernel and reduce pass both on the render stream
+            renderer.render_rows_async(cam.cam, buf.data_ptr(), row0=row0, row_step=step,
+                                       n_rows=n_rows, output=args.output, d_stats_ptr=stats_ptr,
+                                       stream_ptr=stream.cuda_stream)
+            rendered[b].record(stream)
+            coll.wait_event(rendered[b])
+        elif n_rows:
             # the output is completed on the collective stream (rt_render_rows_async_split): the
             # sample kernel runs on the render stream and a direct-mode launch's reduce pass on the
             # collective stream, ahead of this frame's gather, so it overlaps the next frame's
@@ -417,7 +426,8 @@ def run(args):
         dist.barrier()
         gather_ms = (time.perf_counter() - tg) / args.steps * 1e3
     mine = torch.tensor([float(rank), float(n_rows), k_sum / args.steps, r_sum / args.steps, gather_ms,
-                         elapsed / args.steps * 1e3], dtype=torch.float64, device=coll_dev)
+                         elapsed / args.steps * 1e3, float(renderer.workspace_bytes())],
+                        dtype=torch.float64, device=coll_dev)
     if grouped:
         every = [torch.zeros_like(mine) for _ in range(world)]
         dist.all_gather(every, mine)
@@ -425,7 +435,8 @@ def run(args):
         every = [mine]
     per_rank = [{"rank": int(v[0]), "rows": int(v[1]), "kernel_ms_per_frame": round(float(v[2]), 3),
                  "reduce_ms_per_frame": round(float(v[3]), 3), "gather_ms": round(float(v[4]), 3),
-                 "ms_per_step": round(float(v[5]), 3)} for v in (x.cpu() for x in every)]
+                 "ms_per_step": round(float(v[5]), 3),
+                 "workspace_GiB": round(float(v[6]) / 2**30, 3)} for v in (x.cpu() for x in every)]
     st = stats.cpu().tolist()
     rays_per_frame = st[0] / max(1, args.steps)
     samples_per_frame = st[1] / max(1, args.steps)
@@ -509,6 +520,9 @@ def run(args):
                               + (", each frame's gather overlapped with the next frame's render (two row buffers); "
                                  "a direct-mode frame's reduce pass folded by the next frame's drained waves "
                                  "(rt_render_rows_async_deferred)" if args.pipeline == "deferred" else
+                                 ", each frame's gather overlapped with the next frame's render (two row buffers); "
+                                 "a direct-mode reduce pass on the render stream (one per-sample buffer)"
+                                 if args.pipeline == "plain" else
                                  ", each frame's gather and a direct-mode reduce pass on the collective stream, "
                                  "overlapped with the next frame's render (two row buffers; "
                                  "rt_render_rows_async_split)")

@@ -53,6 +53,20 @@ static double hit_sphere(const rt_sphere& s, V o, V d, double tmin, double close
     return r;
 }
 
+// candidate classes of a sphere test at the time the walk runs it (SIM_FAR): 0 no candidate block
+// for this lane (miss, or both roots <= t_min: LeafFilter::behind), 1 a block whose root1 provably
+// lies beyond the running closest (a far filter could drop it), 2 a live candidate
+static int cand_class(const rt_sphere& s, V o, V d, double tmin, double closest) {
+    const V oc = mkv(s.center) - o;
+    const double a = dot(d, d), h = dot(d, oc), c = dot(oc, oc) - s.radius * s.radius;
+    const double disc = h * h - a * c;
+    if (disc < 0) return 0;
+    const double sq = std::sqrt(disc);
+    if ((h + sq) / a <= tmin) return 0;
+    if ((h - sq) / a > closest) return 1;
+    return 2;
+}
+
 struct Ray {
     V o, d;
     double t;  // closest hit (+inf: miss)
@@ -232,6 +246,12 @@ int main(int argc, char** argv) {
     double dead = 0;
     size_t nw = 0;
     std::vector<int> ray_visits(rays.size(), 0);  // inner steps of each ray's walk (SIM_GROUP_ORACLE)
+    // SIM_FAR: wave-level candidate blocks now (any lane with class >= 1) and with a far filter (any
+    // lane with class 2), for the always-list spheres (in list order) and the leaf rounds (a lane's
+    // k-th leaf: one block per round while any lane has a slot left)
+    const bool sim_far = std::getenv("SIM_FAR") != nullptr;
+    std::vector<std::vector<int>> al_cls(64), lf_now(64), lf_far(64);
+    double al_blocks_now = 0, al_blocks_far = 0, lf_blocks_now = 0, lf_blocks_far = 0;
     for (size_t w0 = 0; w0 + 64 <= rays.size(); w0 += 64, ++nw) {
         size_t maxleaf = 0;
         for (int l = 0; l < 64; l++) {
@@ -242,7 +262,13 @@ int main(int argc, char** argv) {
                 continue;
             }
             double closest = INFINITY;
-            for (size_t q = 0; q < na; q++) closest = std::min(closest, hit_sphere(sp[bvh.slot_to_sphere[q]], R.o, R.d, 1e-3, closest));
+            al_cls[l].assign(na, 0);
+            lf_now[l].clear();
+            lf_far[l].clear();
+            for (size_t q = 0; q < na; q++) {
+                if (sim_far) al_cls[l][q] = cand_class(sp[bvh.slot_to_sphere[q]], R.o, R.d, 1e-3, closest);
+                closest = std::min(closest, hit_sphere(sp[bvh.slot_to_sphere[q]], R.o, R.d, 1e-3, closest));
+            }
             const float inv[3] = {1.0f / (float)R.d.x, 1.0f / (float)R.d.y, 1.0f / (float)R.d.z};
             const float org[3] = {(float)R.o.x, (float)R.o.y, (float)R.o.z};
             auto box = [&](const float* lo, const float* hi, float& tn) {
@@ -294,6 +320,18 @@ int main(int argc, char** argv) {
                     run = 0;
                     leaves++;
                     const size_t base = na + (size_t)rtbvh::kLeafMax * (size_t)(~cur);
+                    int n_now = 0, n_far = 0;
+                    if (sim_far) {  // classes against the closest at the round's start (both slots' tests run first)
+                        for (int u = 0; u < rtbvh::kLeafMax; u++) {
+                            const uint32_t k = bvh.slot_to_sphere[base + u];
+                            if (k == rtbvh::kSentinel) continue;
+                            const int c = cand_class(sp[k], R.o, R.d, 1e-3, closest);
+                            n_now += c >= 1;
+                            n_far += c == 2;
+                        }
+                        lf_now[l].push_back(n_now);
+                        lf_far[l].push_back(n_far);
+                    }
                     for (int u = 0; u < rtbvh::kLeafMax; u++) {
                         const uint32_t k = bvh.slot_to_sphere[base + u];
                         if (k == rtbvh::kSentinel) continue;
@@ -308,6 +346,24 @@ int main(int argc, char** argv) {
             maxleaf = std::max(maxleaf, runs[l].size() - 1);
         }
         wave_leaf += (double)maxleaf;
+        if (sim_far) {
+            for (size_t q = 0; q < na; q++) {
+                bool any_now = false, any_far = false;
+                for (int l = 0; l < 64; l++) {
+                    any_now |= al_cls[l].size() > q && al_cls[l][q] >= 1;
+                    any_far |= al_cls[l].size() > q && al_cls[l][q] == 2;
+                }
+                al_blocks_now += any_now;
+                al_blocks_far += any_far;
+            }
+            for (size_t k = 0; k < maxleaf; k++) {  // leaf round k: blocks = max slots left over lanes
+                int mn = 0, mf = 0;
+                for (int l = 0; l < 64; l++)
+                    if (k < lf_now[l].size()) { mn = std::max(mn, lf_now[l][k]); mf = std::max(mf, lf_far[l][k]); }
+                lf_blocks_now += mn;
+                lf_blocks_far += mf;
+            }
+        }
         for (size_t k = 0; k <= maxleaf; k++) {
             int m = 0;
             for (int l = 0; l < 64; l++)
@@ -598,6 +654,9 @@ int main(int argc, char** argv) {
     }
 
     const double nr = (double)nw * 64;
+    if (sim_far)
+        std::fprintf(stderr, "far filter (lockstep waves of 64 rays): candidate blocks per wave: always-list %.3f -> %.3f, "
+                     "leaf rounds %.3f -> %.3f\n", al_blocks_now / nw, al_blocks_far / nw, lf_blocks_now / nw, lf_blocks_far / nw);
     std::printf("{\"nodes\": %zu, \"depth\": %d, \"n_always\": %zu, \"visits_per_ray\": %.4f, \"leaves_per_ray\": %.4f, "
                 "\"leaf_tests_per_ray\": %.4f, \"wave_inner_steps\": %.3f, \"wave_leaf_rounds\": %.3f, \"dead_pops_per_ray\": %.4f}\n",
                 bvh.nodes.size(), bvh.depth, na, visits / nr, leaves / nr, tests / nr, wave_steps / nw, wave_leaf / nw, dead / nr);

@@ -43,7 +43,7 @@ ap.add_argument("--pipe-frames", type=int, default=0,
                 help="also time each rank's rows in bench.py's frame pipeline (two row buffers, render "
                      "stream, output completed on a second stream: rt_render_rows_async_split), this many "
                      "frames, wall clock per frame")
-ap.add_argument("--pipe-mode", choices=["split", "deferred"], default="deferred",
+ap.add_argument("--pipe-mode", choices=["plain", "split", "deferred"], default="deferred",
                 help="the pipeline's render call (bench.py --pipeline)")
 args = ap.parse_args()
 
@@ -81,8 +81,17 @@ def pipeline_ms(row0, step, n_rows):
         for wb in ((b, pb) if pend[0] else (b,)):
             if freed[wb] is not None:
                 render.wait_event(freed[wb])
-        r.render_rows_async(cam.cam, outs[b].data_ptr(), row0=row0, row_step=step, n_rows=n_rows,
-                            stream_ptr=render.cuda_stream, out_stream_ptr=coll.cuda_stream, deferred=deferred)
+        if args.pipe_mode == "plain":
+            # one per-sample buffer: the reduce pass runs on the render stream after the sample
+            # kernel; the collective stream waits for the frame
+            r.render_rows_async(cam.cam, outs[b].data_ptr(), row0=row0, row_step=step, n_rows=n_rows,
+                                stream_ptr=render.cuda_stream)
+            done = torch.cuda.Event()
+            done.record(render)
+            coll.wait_event(done)
+        else:
+            r.render_rows_async(cam.cam, outs[b].data_ptr(), row0=row0, row_step=step, n_rows=n_rows,
+                                stream_ptr=render.cuda_stream, out_stream_ptr=coll.cuda_stream, deferred=deferred)
         if pend[0]:
             freed[pb] = torch.cuda.Event()
             freed[pb].record(coll)
