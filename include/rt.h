@@ -219,8 +219,9 @@ int rt_context_kernel_times_total(rt_context* ctx, double* sample_ms, double* re
  * the parts of [4]: wave-cycles finalising units, handing out items (claims), seeding + getRay;
  * [26..31] wave-level executions: loop iterations, rejection trips, seeding blocks, walks started
  * (always-list tests), shading blocks, unit finalisations}, [32] wave-level seed-window passes
- * and [33] the second passes among them (-DRTZIG_SEED_WINDOW=1 builds; 0 otherwise), [34..39]
- * reserved (0).  Counts 0-3 are exact and deterministic;
+ * and [33] the second passes among them, [34..39] reserved.  Words 32..39 are written only by
+ * -DRTZIG_SEED_WINDOW=1 builds: the default library writes words 0..31, so a 32-word buffer (the
+ * size before round 5) stays valid for it.  Counts 0-3 are exact and deterministic;
  * the cycles and wave-level counts are diagnostics. */
 int rt_context_enable_profile(rt_context* ctx, int enable);
 

@@ -1789,8 +1789,10 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
                 atomicAdd(&stats[29], (unsigned long long)n_wstart);
                 atomicAdd(&stats[30], (unsigned long long)n_shade);
                 atomicAdd(&stats[31], (unsigned long long)n_fin);
-                atomicAdd(&stats[32], (unsigned long long)n_win);
-                atomicAdd(&stats[33], (unsigned long long)n_win2);
+                if constexpr (kSeedWindow) {  // a default build writes words 0..31 only (rt.h)
+                    atomicAdd(&stats[32], (unsigned long long)n_win);
+                    atomicAdd(&stats[33], (unsigned long long)n_win2);
+                }
             }
         }
     }
