@@ -83,17 +83,19 @@ def test_hip_ranks_gather_equals_single_rank(oracle, world, mode):
     assert np.array_equal(img, ref)
 
 
-def test_bench_pipelined_gather_bit_exact():
+@pytest.mark.parametrize("pipeline", ["deferred", "split", "plain"])
+def test_bench_pipelined_gather_bit_exact(pipeline):
     """bench.py's own timed loop over 2 ranks it starts itself (gloo rehearsal, both on GPU 0): two
     row buffers, a render stream and the collective stream, each frame's gather overlapped with the
-    next frame's render.  `--check` compares rank 0's last gathered frame with a whole-image render
-    bit for bit (the pipelining must not let a render overwrite rows still being gathered)."""
+    next frame's render, in each --pipeline (deferred: the default; split; plain: one per-sample
+    buffer).  `--check` compares rank 0's last gathered frame with a whole-image render bit for bit
+    (the pipelining must not let a render overwrite rows still being gathered)."""
     import json
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     args = ["--gpus", "2", "--dist-backend", "gloo", "--check", "--steps", "4", "--warmup", "1", "--spp", "8",
-            "--width", "240", "--no-cpu-baseline", "--no-fast", "--no-dropin"]
+            "--width", "240", "--no-cpu-baseline", "--no-fast", "--no-dropin", "--pipeline", pipeline]
     p = subprocess.run([sys.executable, os.path.join(root, "bench.py")] + args, capture_output=True, text=True,
                        timeout=110, cwd=root)
     assert p.returncode == 0, p.stderr[-2000:]
