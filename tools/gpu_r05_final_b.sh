@@ -6,6 +6,9 @@
 cd "$GRAFT_REPO_ROOT" || exit 2
 mkdir -p gpurun_out
 T=${TAG:-r05}
+# the bench line again, now reading the round's own PMC summary (profiles/pmc_traffic.json)
+timeout -k 10 300 python3 -u bench.py > gpurun_out/bench_${T}_final.json 2> gpurun_out/bench_${T}_final.err
+rc=$?; echo "bench rc=$rc"; cat gpurun_out/bench_${T}_final.json; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 240 python3 -u tools/dropin_cold.py --runs 3 --configs 2,4,5 > gpurun_out/dropin_cold_$T.json 2> gpurun_out/dropin_cold_$T.err
 rc=$?; echo "dropin rc=$rc"; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python3 -u tools/rank_sim.py --ns 1 2 4 8 --reps 2 --pipe-frames 8 --pipe-mode deferred > gpurun_out/ranksim_deferred_$T.json 2> gpurun_out/ranksim_deferred_$T.err
