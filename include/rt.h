@@ -31,7 +31,7 @@ extern "C" {
 
 #define RT_ABI_VERSION 3
 /* uint64 words of the d_stats buffer of an instrumented render (rt_context_enable_profile) */
-#define RT_PROFILE_STATS_WORDS 40
+#define RT_PROFILE_STATS_WORDS 32
 
 /* ---- status codes ---------------------------------------------------------------------------- */
 typedef enum rt_status {
@@ -208,7 +208,7 @@ int rt_context_kernel_times(rt_context* ctx, double* sample_ms, double* reduce_m
  * *n_launches = the number of sample-kernel launches summed. */
 int rt_context_kernel_times_total(rt_context* ctx, double* sample_ms, double* reduce_ms, uint32_t* n_launches);
 /* Instrumented kernels (diagnostics): when enabled, `d_stats` of rt_render_rows_async must hold
- * RT_PROFILE_STATS_WORDS (40) uint64: {rays, samples, sphere tests executed, BVH node visits, wave-cycles in queue refill,
+ * RT_PROFILE_STATS_WORDS (32) uint64: {rays, samples, sphere tests executed, BVH node visits, wave-cycles in queue refill,
  * wave-cycles in the closest-hit walk, wave-cycles in shading, wave-iterations of the BVH inner
  * (internal-node) loop, wave-iterations of BVH leaf rounds, wave-level candidate blocks (sqrt +
  * root division), wave-level second-root divisions, node visits of camera rays, sphere tests of
@@ -218,10 +218,7 @@ int rt_context_kernel_times_total(rt_context* ctx, double* sample_ms, double* re
  * waves of (wave end - the wave's first empty claim), [22] the last wave's first empty claim, [23..25]
  * the parts of [4]: wave-cycles finalising units, handing out items (claims), seeding + getRay;
  * [26..31] wave-level executions: loop iterations, rejection trips, seeding blocks, walks started
- * (always-list tests), shading blocks, unit finalisations}, [32] wave-level seed-window passes
- * and [33] the second passes among them, [34..39] reserved.  Words 32..39 are written only by
- * -DRTZIG_SEED_WINDOW=1 builds: the default library writes words 0..31, so a 32-word buffer (the
- * size before round 5) stays valid for it.  Counts 0-3 are exact and deterministic;
+ * (always-list tests), shading blocks, unit finalisations}.  Counts 0-3 are exact and deterministic;
  * the cycles and wave-level counts are diagnostics. */
 int rt_context_enable_profile(rt_context* ctx, int enable);
 

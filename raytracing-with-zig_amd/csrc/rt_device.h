@@ -216,20 +216,6 @@ __host__ __device__ __forceinline__ uint64_t sm_mix_hd(uint64_t x) {
 struct Rng {
     uint64_t s0, s1, s2, s3;
 
-    // the state to / from a seed window entry (4 x u64, two 16-byte accesses)
-    __device__ __forceinline__ void store(uint64_t* p) const {
-        typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
-        *(u64x2*)p = u64x2{s0, s1};
-        *(u64x2*)(p + 2) = u64x2{s2, s3};
-    }
-    __device__ __forceinline__ void load(const uint64_t* p) {
-        typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
-        const u64x2 a = *(const u64x2*)p, b = *(const u64x2*)(p + 2);
-        s0 = a.x;
-        s1 = a.y;
-        s2 = b.x;
-        s3 = b.y;
-    }
     // DefaultPrng.init(key): Xoshiro256.seed via SplitMix64 (zig std/Random/Xoshiro256.zig)
     __device__ __forceinline__ void seed(uint64_t key) {
         uint64_t sm = key;

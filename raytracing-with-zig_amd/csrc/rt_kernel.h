@@ -49,22 +49,7 @@ constexpr uint32_t kUnitS = RTZIG_UNIT_S;  // samples per unit of the main chunk
 constexpr uint32_t kSlots = RTZIG_SLOTS;   // units a wave holds at once (48 x 2 measured best)
 constexpr uint32_t kSlotMask = (1u << kSlots) - 1;
 constexpr uint32_t kRingSlotDoubles = kUnitS * 64 * 3;
-// The seed window (path_loop): for 64 consecutive items of a wave's hand-out order, the Xoshiro256++
-// state after getRay's sampleSquare draws and the camera ray's direction (or pixel sample point),
-// computed by all 64 lanes at once and read back by the lanes handed those items.  It sits
-// after the wave's ring slots (ring mode) or alone (direct mode: ua.ring then holds only the windows).
-// RTZIG_SEED_WINDOW (an A/B knob, default 0 — measured and not adopted): 1 builds it;
-// 0: each fresh lane seeds its own generator and the workspace holds no windows.
-#ifndef RTZIG_SEED_WINDOW
-#define RTZIG_SEED_WINDOW 0
-#endif
-constexpr bool kSeedWindow = RTZIG_SEED_WINDOW != 0;
-constexpr uint32_t kSeedEntryWords = 8;  // per item: generator state (4 x u64) + camera ray direction (<= 3 x f64)
-constexpr uint32_t kSeedWindowDoubles = 64 * kSeedEntryWords;  // one window slot: 4 KiB
-constexpr uint32_t kSeedWindowSlots = kSeedWindow ? 2 : 0;    // double-buffered
-constexpr uint32_t kRingWaveDoubles = kSlots * kRingSlotDoubles + kSeedWindowSlots * kSeedWindowDoubles;  // 144 KiB per wave (+8 with windows)
-// ua.ring's stride per wave (direct mode without windows: none, ua.ring is null)
-constexpr uint32_t ring_wave_doubles(bool direct) { return direct ? kSeedWindowSlots * kSeedWindowDoubles : kRingWaveDoubles; }
+constexpr uint32_t kRingWaveDoubles = kSlots * kRingSlotDoubles;  // 144 KiB of f64 per wave
 // counters: ring mode's claim counter ctr[0]; direct mode one per queue segment, each on its own
 // 128-B line, ctr[kCtrStride * seg] — zeroed per launch (the first kCtrLaunchBytes) — then the
 // STICKY error word ctr[kErrWord]: set by a wave that gave up waiting (rt_units.h), cleared only by

@@ -95,21 +95,6 @@ __device__ __forceinline__ bool camera_start(uint32_t i, uint32_t j, Rng& g, Ray
     r.dir = ps;
     return true;  // the disk sample is pending
 }
-// The camera ray of a seed-window entry (path_loop): origin = center and the pending disk sample of
-// camera_start, for a direction computed when the window was made.
-__device__ __forceinline__ bool camera_origin(Ray& r) {
-    u32x8 A;  // dwords 6..13: center (+2 unused)
-    u32x2 C;  // dwords 42..43: defocus_angle
-    const uint64_t kp = (uint64_t)__builtin_amdgcn_kernarg_segment_ptr();
-    asm volatile(
-        "s_load_dwordx8 %0, %2, 24\n\t"
-        "s_load_dwordx2 %1, %2, 168\n\t"
-        "s_waitcnt lgkmcnt(0)"
-        : "=s"(A), "=s"(C)
-        : "s"(kp));
-    r.orig = mk(dw2d(A[0], A[1]), dw2d(A[2], A[3]), dw2d(A[4], A[5]));
-    return !(dw2d(C[0], C[1]) <= 0);
-}
 // rayOrigin = defocusDiskSample() = (center + defocusDiskU * p.x) + defocusDiskV * p.y;
 // rayDirection = pixelSample - rayOrigin
 __device__ __forceinline__ void camera_finish(double px, double py, Ray& r) {
@@ -210,19 +195,6 @@ __device__ __forceinline__ bool camera_start(uint32_t i, uint32_t j, Rng& g, fm:
     }
     r.dir = ps;
     return true;
-}
-__device__ __forceinline__ bool camera_origin(fm::Ray& r) {
-    u32x4 A;  // fcam[0..3]
-    u32x4 B;  // fcam[16..19]
-    const uint64_t kp = (uint64_t)__builtin_amdgcn_kernarg_segment_ptr();
-    asm volatile(
-        "s_load_dwordx4 %0, %2, %3\n\t"
-        "s_load_dwordx4 %1, %2, %4\n\t"
-        "s_waitcnt lgkmcnt(0)"
-        : "=s"(A), "=s"(B)
-        : "s"(kp), "i"(kFcam), "i"(kFcam + 64));
-    r.orig = fm::mk(fw(A[0]), fw(A[1]), fw(A[2]));
-    return !(fw(B[2]) <= 0);
 }
 __device__ __forceinline__ void camera_finish(float px, float py, fm::Ray& r) {
 #pragma clang fp contract(fast)
@@ -427,8 +399,6 @@ constexpr int kRefetchK = RTZIG_REFETCH_K;
 // left to fetch) and its rejection loops run until every lane has its sample instead of kRuvTrips
 // trips per iteration, so the paths still in flight at the end of a launch take fewer loop
 // iterations (the drain tail).  Results unchanged.
-// Seed window (RTZIG_SEED_WINDOW, rt_kernel.h, default 0): path_loop precomputes the generator
-// states of the wave's next 64 items with every lane (see there).
 #ifndef RTZIG_DRAIN
 #define RTZIG_DRAIN 0
 #endif
@@ -1185,50 +1155,6 @@ __device__ __forceinline__ void shade_f32(int k, float t, const GeoRec* __restri
     }
 }
 
-// ds_bpermute (the LDS crossbar, no LDS storage): each lane gets `v` of lane src_bytes / 4
-__device__ __forceinline__ uint64_t permute64(int src_bytes, uint64_t v) {
-    const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_bpermute(src_bytes, (int)(uint32_t)v);
-    const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_bpermute(src_bytes, (int)(uint32_t)(v >> 32));
-    return ((uint64_t)hi << 32) | lo;
-}
-__device__ __forceinline__ double permute1(int src_bytes, double v) {
-    return __builtin_bit_cast(double, permute64(src_bytes, __builtin_bit_cast(uint64_t, v)));
-}
-__device__ __forceinline__ float permute1(int src_bytes, float v) {
-    return __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(src_bytes, __builtin_bit_cast(int, v)));
-}
-__device__ __forceinline__ v3 permute_v(int src_bytes, const v3& v) {
-    return mk(permute1(src_bytes, v.x), permute1(src_bytes, v.y), permute1(src_bytes, v.z));
-}
-__device__ __forceinline__ fm::f3 permute_v(int src_bytes, const fm::f3& v) {
-    return fm::mk(permute1(src_bytes, v.x), permute1(src_bytes, v.y), permute1(src_bytes, v.z));
-}
-// Seed-window entries (path_loop): generator state + camera ray direction, 64 B
-__device__ __forceinline__ void win_store(uint64_t* e, const Rng& g, const v3& d) {
-    typedef double f64x2 __attribute__((ext_vector_type(2)));
-    g.store(e);
-    *(f64x2*)(e + 4) = f64x2{d.x, d.y};
-    *(double*)(e + 6) = d.z;
-}
-__device__ __forceinline__ void win_load(const uint64_t* e, Rng& g, v3& d) {
-    typedef double f64x2 __attribute__((ext_vector_type(2)));
-    g.load(e);
-    const f64x2 xy = *(const f64x2*)(e + 4);
-    d = mk(xy.x, xy.y, *(const double*)(e + 6));
-}
-__device__ __forceinline__ void win_store(uint64_t* e, const Rng& g, const fm::f3& d) {
-    typedef float f32x2 __attribute__((ext_vector_type(2)));
-    g.store(e);
-    *(f32x2*)(e + 4) = f32x2{d.x, d.y};
-    *(float*)(e + 5) = d.z;
-}
-__device__ __forceinline__ void win_load(const uint64_t* e, Rng& g, fm::f3& d) {
-    typedef float f32x2 __attribute__((ext_vector_type(2)));
-    g.load(e);
-    const f32x2 xy = *(const f32x2*)(e + 4);
-    d = fm::mk(xy.x, xy.y, *(const float*)(e + 5));
-}
-
 // Direct mode's reduce pass for one pixel (reduce_kernel, and the deferred fold below).
 __device__ __forceinline__ void reduce_pixel(const double* __restrict__ samples, uint32_t P, uint32_t spp, uint32_t q,
                                              void* out, uint32_t format, double scale) {
@@ -1311,7 +1237,7 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
     // wave-level executions (kProf only; scalar, wave-uniform): loop iterations, trip-loop trips, seeding
     // blocks, walks started (always-list tests), shading blocks, finalisations — with the per-step counts
     // of Prof they weight the static instruction counts of each region (tools/region_table.py)
-    uint32_t n_iter = 0, n_trip = 0, n_seed = 0, n_wstart = 0, n_shade = 0, n_fin = 0, n_win = 0, n_win2 = 0;
+    uint32_t n_iter = 0, n_trip = 0, n_seed = 0, n_wstart = 0, n_shade = 0, n_fin = 0;
     uint64_t rt_start = 0, rt_drain = 0;  // s_memrealtime (100 MHz) at start / first empty claim (kProf only)
     if constexpr (kProf) rt_start = __builtin_amdgcn_s_memrealtime();
 
@@ -1349,135 +1275,8 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
         }
         // the lanes handed an item above start their path: seeding and getRay run once, outside
         // the claim loop, so the generator state and ray are not loop-carried through it
-        RTK_MARK("seed");
         if constexpr (kProf) n_seed += __ballot(fresh) != 0 ? 1u : 0u;
-#if RTZIG_SEED_WINDOW
-        // Seed window.  A path's generator is DefaultPrng.init(key) for its (pixel, sample) key —
-        // five SplitMix64 mixes — and getRay then draws sampleSquare's offsets and forms the pixel
-        // sample point: ~600 issue cycles of 64-bit multiplies, shifts and f64 math, which the ~21
-        // lanes handed an item per iteration ran as a wave-level block every iteration (1/3 of the
-        // lanes busy).  Instead all 64 lanes compute those values for the 64 consecutive items of
-        // the current unit (claim) that start at the lowest item not yet covered: the lanes handed
-        // one of them now take it from the computing lane by ds_bpermute (no memory round trip),
-        // and the whole window is stored for the lanes handed the others over the next iterations.
-        // The values, and so the bits, are unchanged.
-        // Two window slots per wave: a pass stores into the slot the iteration's loads did not read.
-        // Ordering needs no s_waitcnt: a wave's vector memory operations are performed in order
-        // (the AMDGPU memory model's wavefront scope, which LLVM implements with no wait at all),
-        // so a later iteration's loads see this pass's stores; the wavefront-scope fences keep the
-        // compiler from moving the window's loads and stores across each other.  The items handed in one
-        // iteration come from at most two units (claims) in the common case, each a consecutive run;
-        // a lane holding an item of the previous unit (the refill switched units under it) is served
-        // by a pass of its own whose window is not kept.
-        {
-            const uint32_t wb = us.win_base & 0x7fffffffu;  // bit 31: the slot holding the window
-            const uint32_t wslot = us.win_base >> 31;
-            uint64_t* const win0 = us.seeds();
-            bool seeded = false;
-            // what the passes hand over, merged into g / r.dir after them: written there directly, the
-            // pass would first wait for the window loads into the same registers (a VGPR
-            // write-after-write waits for the load whatever the lanes)
-            Rng pg;  // (read only where handed)
-            V pdir;
-            bool handed = false;
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            if (fresh && us.current(myslot) && mi - wb < 64u) {
-                win_load(win0 + kSeedWindowDoubles * wslot + kSeedEntryWords * (mi - wb), g, r.dir);
-                seeded = true;
-            }
-            // unrolled: as a runtime loop the pass kept enough SGPRs live to spill 23 more kernarg
-            // values into VGPR lanes, reloaded in the walk setup and shading
-#pragma unroll
-            for (int pass = 0; pass < 2; ++pass) {
-                const uint64_t need = __ballot(fresh && !seeded);
-                if (need == 0) break;
-                if constexpr (kProf) {
-                    ++n_win;
-                    n_win2 += pass;
-                }
-                if (pass == 0) {
-                    RTK_MARK("seed_window");
-                } else {
-                    RTK_MARK("seed_window2");
-                }
-                const uint32_t l0 = (uint32_t)__builtin_ctzll(need);
-                const uint32_t base = __builtin_amdgcn_readlane(mi, l0);
-                const bool cur_unit = __builtin_amdgcn_readlane((uint32_t)us.current(myslot), l0) != 0;
-                const uint32_t m = base + lane;  // this lane's window item
-                uint32_t wq, wsmp;
-                if constexpr (kDirect) {
-                    wsmp = fastdiv(m, ua.div_p);
-                    wq = m - wsmp * ua.P;
-                } else {
-                    // unit items: pixel 64 * tile + m % 64, sample s0 + m / 64 (refill), taken
-                    // relative to the lowest missing lane's own item
-                    const uint32_t q0 = __builtin_amdgcn_readlane(fq, l0), s0 = __builtin_amdgcn_readlane(fs, l0);
-                    wq = (q0 - (base & 63u)) + (m & 63u);
-                    wsmp = (s0 - (base >> 6)) + (m >> 6);
-                }
-                // items past the unit's (claim's) end are computed too and never read.  Each entry
-                // also takes getRay's first part: sampleSquare's two draws and the pixel sample
-                // point (camera_start), leaving the state where the path continues from.
-                const uint32_t wrow = fastdiv(wq, p.div_width);
-                const uint32_t wi = wq - wrow * W, wj = p.row0 + wrow * p.row_step;
-                Rng t;
-                t.seed(sample_key(p.seed_mix, (uint64_t)wj * W + wi, wsmp));
-                RayT wr;
-                (void)camera_start(wi, wj, t, wr);
-                // a window of the current unit is kept, in the slot this iteration did not read; a
-                // second kept pass (direct mode: a second claim; ring mode: after a pass for the
-                // previous unit, whose window is not kept) writes the slot the first one did or,
-                // after an unkept one, slot 1 — in order after this iteration's loads of it
-                if (cur_unit) {
-                    const uint32_t ns = (pass == 0) ? (wslot ^ 1u) : (us.win_base >> 31);
-                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                    win_store(win0 + kSeedWindowDoubles * ns + kSeedEntryWords * lane, t, wr.dir);
-                    us.win_base = (ns << 31) | base;
-                } else {
-                    us.win_base = kNoWindow;
-                }
-                // the lanes handed one of these items take it from the lane that computed it
-                const bool take = fresh && !seeded && us.current(myslot) == cur_unit && mi - base < 64u;
-                const int src = (int)((mi - base) & 63u) * 4;
-                t.s0 = permute64(src, t.s0);
-                t.s1 = permute64(src, t.s1);
-                t.s2 = permute64(src, t.s2);
-                t.s3 = permute64(src, t.s3);
-                wr.dir = permute_v(src, wr.dir);
-                if (take) {
-                    pg = t;
-                    pdir = wr.dir;
-                    seeded = true;
-                    handed = true;
-                }
-            }
-            // rare: items of a third unit (claim) in one refill — tiny units at a launch's end, or
-            // partial tiles — seed their own generators, as without the window
-            if (__builtin_expect(__ballot(fresh && !seeded) != 0, 0)) {
-                RTK_MARK("rare");
-                if (fresh && !seeded) {
-                    const uint32_t row_local = fastdiv(fq, p.div_width);
-                    const uint32_t i = fq - row_local * W;
-                    const uint32_t j = p.row0 + row_local * p.row_step;
-                    pg.seed(sample_key(p.seed_mix, (uint64_t)j * W + i, fs));
-                    RayT sr;
-                    (void)camera_start(i, j, pg, sr);
-                    pdir = sr.dir;
-                    handed = true;
-                }
-            }
-            if (handed) {
-                g = pg;
-                r.dir = pdir;
-            }
-            RTK_MARK("seed");
-        }
-        if (fresh) {
-            dpend = camera_origin(r);  // the entry holds the direction (camera_start)
-            att = V{1, 1, 1};
-            bounce = 0;
-        }
-#else
+        RTK_MARK("seed");
         if (fresh) {
             const uint32_t row_local = fastdiv(fq, p.div_width);
             const uint32_t i = fq - row_local * W;
@@ -1488,7 +1287,6 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
             att = V{1, 1, 1};
             bounce = 0;
         }
-#endif
         if constexpr (kProf) cyc_seed += __builtin_amdgcn_s_memtime() - t_ref;
         RTK_MARK("idle");
         const bool idle = __ballot(active) == 0;
@@ -1789,10 +1587,6 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
                 atomicAdd(&stats[29], (unsigned long long)n_wstart);
                 atomicAdd(&stats[30], (unsigned long long)n_shade);
                 atomicAdd(&stats[31], (unsigned long long)n_fin);
-                if constexpr (kSeedWindow) {  // a default build writes words 0..31 only (rt.h)
-                    atomicAdd(&stats[32], (unsigned long long)n_win);
-                    atomicAdd(&stats[33], (unsigned long long)n_win2);
-                }
             }
         }
     }

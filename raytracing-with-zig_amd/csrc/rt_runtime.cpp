@@ -909,18 +909,10 @@ int render_rows(rt_context* ctx, const rt_camera* cam, uint32_t output_format, u
     // mode alternate two per-sample buffers
     const bool split_reduce = direct && split;
     uint32_t sbuf = 0;
-    // ua.ring holds, per resident wave of the kernel this call launches, its two ring slots (ring
-    // mode) and, in a -DRTZIG_SEED_WINDOW=1 build, its seed windows (both modes, rt_kernel.h)
-    uint32_t waves = 0;
-    HIP_CHECK(launch(&ua, &waves));
-    waves = std::max(waves, 1u);
-    const size_t wave_bytes = (size_t)rtk::ring_wave_doubles(direct) * sizeof(double);
     if (direct) {
-        rc = release_buffer(ctx, (void**)&ctx->d_sums, &ctx->sums_bytes);
-        // a ring-mode ring is given back (for the windows alone, if built)
-        if (!rc && wave_bytes == 0) rc = release_buffer(ctx, (void**)&ctx->d_ring, &ctx->ring_bytes);
-        if (!rc && wave_bytes) rc = fit_buffer(ctx, (void**)&ctx->d_ring, &ctx->ring_bytes, (size_t)waves * wave_bytes);
-        ctx->ring_waves = (rc || !wave_bytes) ? 0u : (uint32_t)(ctx->ring_bytes / wave_bytes);
+        rc = release_buffer(ctx, (void**)&ctx->d_ring, &ctx->ring_bytes);
+        if (!rc) rc = release_buffer(ctx, (void**)&ctx->d_sums, &ctx->sums_bytes);
+        ctx->ring_waves = 0;
         if (!rc) rc = fit_buffer(ctx, (void**)&ctx->d_samples, &ctx->samples_bytes, direct_bytes);
         if (split_reduce) {
             if (!rc) rc = fit_buffer(ctx, (void**)&ctx->d_samples2, &ctx->samples2_bytes, direct_bytes);
@@ -932,12 +924,15 @@ int render_rows(rt_context* ctx, const rt_camera* cam, uint32_t output_format, u
         }
     } else {
         // the ring holds the persistent grid of the kernel this call launches (its resident waves)
+        uint32_t waves = 0;
+        HIP_CHECK(launch(&ua, &waves));
+        waves = std::max(waves, 1u);
+        constexpr size_t kWaveBytes = rtk::kRingWaveDoubles * sizeof(double);
         rc = release_buffer(ctx, (void**)&ctx->d_samples, &ctx->samples_bytes);
         if (!rc) rc = release_buffer(ctx, (void**)&ctx->d_samples2, &ctx->samples2_bytes);
         ctx->samples_flip = 0;
-        // a direct-mode ring (windows only, if built) is too small: fit_buffer reallocates it
-        if (!rc) rc = fit_buffer(ctx, (void**)&ctx->d_ring, &ctx->ring_bytes, (size_t)waves * wave_bytes);
-        ctx->ring_waves = rc ? 0u : (uint32_t)(ctx->ring_bytes / wave_bytes);
+        if (!rc) rc = fit_buffer(ctx, (void**)&ctx->d_ring, &ctx->ring_bytes, (size_t)waves * kWaveBytes);
+        ctx->ring_waves = rc ? 0u : (uint32_t)(ctx->ring_bytes / kWaveBytes);
         if (!rc && ua.n_chunks > 1) rc = fit_buffer(ctx, (void**)&ctx->d_sums, &ctx->sums_bytes, P * 3 * sizeof(double));
     }
     const size_t flag_bytes = (n_tiles * sizeof(uint32_t) + 15) & ~(size_t)15;  // memset in 16-B multiples
@@ -956,7 +951,7 @@ int render_rows(rt_context* ctx, const rt_camera* cam, uint32_t output_format, u
     }
     if (rc) return rc;
     trace_mark("workspace_alloc");
-    ua.ring = (direct && !rtk::kSeedWindow) ? nullptr : ctx->d_ring;
+    ua.ring = direct ? nullptr : ctx->d_ring;
     ua.sums = direct ? nullptr : ctx->d_sums;
     ua.samples = direct ? (sbuf ? ctx->d_samples2 : ctx->d_samples) : nullptr;
     ua.spp = cam->samples_per_pixel;

@@ -63,12 +63,6 @@ __device__ __forceinline__ uint32_t wait_clock() { return (uint32_t)(__builtin_a
 // Wave-uniform scheduler state (every member is the same in all 64 lanes).  kDirect: direct mode
 // (rt_kernel.h): guided claims of flat items t = s * P + q (also the item's index in ua.samples);
 // no slots, no finalisation.
-// "No seed window": the membership test is `item - win_base < 64` in 32-bit arithmetic, so the empty
-// window must be a base no item lies within 64 above: item ids stay far below 2^32 - 64 (ring mode:
-// < 64 x kUnitS; direct mode: P x spp < 16 GiB / 24 B, rt_runtime.cpp).  (~0u would match items
-// 0..62.)
-constexpr uint32_t kNoWindow = 0xffffffc0u;  // (bit 31 is the slot bit: items stay below 2^31 - 64)
-
 template <bool kDirect>
 struct UnitSched {
     const UnitArgs& ua;
@@ -86,14 +80,9 @@ struct UnitSched {
     uint32_t n_dep_wait = 0;   // diagnostics (instrumented build): finalisations deferred on a flag
     uint32_t n_no_slot = 0;    // ... refills stopped for want of a free slot
     bool drained = false;            // the claim counter is exhausted
-    // the seed window (path_loop): generator states of the current unit's (claim's) items
-    // [win_base, win_base + 64); kNoWindow: none.  A claim empties it (ring mode: the window always
-    // belongs to the unit being handed out; direct mode: item ids are global, but a new claim's
-    // items lie elsewhere anyway)
-    uint32_t win_base = kNoWindow;  // bit 31: which of the wave's two window slots holds it
     bool failed = false;             // stall bound reached (reported in ctr[kErrWord])
 
-    __device__ UnitSched(const UnitArgs& a, uint32_t wave) : ua(a), ring(a.ring + (size_t)wave * ring_wave_doubles(kDirect)) {
+    __device__ UnitSched(const UnitArgs& a, uint32_t wave) : ua(a), ring(a.ring + (size_t)wave * kRingWaveDoubles) {
         if constexpr (kBounds && !kDirect) {
             if (!bounds_ok(wave < a.ring_waves, a.ctr)) ring = a.ring;
         }
@@ -109,12 +98,6 @@ struct UnitSched {
     __device__ __forceinline__ uint32_t seg_lo(uint32_t g) const {
         return (uint32_t)((uint64_t)ua.n_units * g / kSegs);
     }
-    // this wave's seed window: after its ring slots (ring mode), alone (direct mode)
-    __device__ __forceinline__ uint64_t* seeds() const {
-        return (uint64_t*)(ring + (kDirect ? 0u : kSlots * kRingSlotDoubles));
-    }
-    // a lane's item m (refill's mi) is in the current unit (claim)
-    __device__ __forceinline__ bool current(uint32_t slot) const { return kDirect || slot == cur_slot; }
     __device__ __forceinline__ bool can_claim() const { return !drained && (kDirect || (~busy & kSlotMask) != 0); }
 
     // Claims the next unit into a free slot and makes it the one handed out; false if there is no
@@ -134,7 +117,6 @@ struct UnitSched {
                 t = lo + __builtin_amdgcn_readfirstlane(t);
                 if (t < hi) {
                     wait_t0 = 0;
-                    win_base = kNoWindow;
                     seen = t + k;
                     cur = t;
                     end = hi - t < k ? hi : t + k;
@@ -169,7 +151,6 @@ struct UnitSched {
         busy |= 1u << js;
         cur_slot = js;
         wait_t0 = 0;
-        win_base = kNoWindow;
         cur = 0;
         end = n * 64;
         cur_tile = tile;

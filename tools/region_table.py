@@ -193,7 +193,8 @@ def main():
     sc = args.spp_scale
     n = {"iter": raw[26] * sc, "trips": raw[27] * sc, "seed": raw[28] * sc, "wstart": raw[29] * sc, "shade": raw[30] * sc,
          "inner": raw[7] * sc, "leaf": raw[8] * sc, "cand": raw[9] * sc, "root2": raw[10] * sc, "fin": raw[31] * sc,
-         # seed-window passes (round 5; older profiles have 32 words: estimated as one per 64 samples)
+         # seed-window passes: only the -DRTZIG_SEED_WINDOW=1 build of commit 2b16cfb has these regions
+         # and counts ([32], [33] of its 40-word stats); otherwise estimated as one per 64 samples
          "win": (raw[32] - raw[33] if len(raw) > 33 and raw[32] else raw[1] / 64) * sc,
          "win2": (raw[33] if len(raw) > 33 and raw[32] else raw[1] / 64 / 50) * sc}
     lines = open(args.asm).read().split("\n") if args.asm else asm(["-DRTZIG_MARKS=1"] + ["-D" + d for d in args.D])
