@@ -654,6 +654,44 @@ int main(int argc, char** argv) {
     }
 
     const double nr = (double)nw * 64;
+    // SIM_ALWAYS: wave-level candidate blocks of the always-list tests under other schedules, from
+    // the rays' lockstep waves: "seq" = one block per sphere any lane needs (the kernel's), "pairs" =
+    // the leaf rounds' compaction over sphere pairs (0,1),(2,3) of the order, "full" = one block per
+    // round over all spheres; "far" drops candidates whose root1 lies beyond the running closest;
+    // orders: the list's, and the ground (the largest) last
+    if (std::getenv("SIM_ALWAYS") && na == 4) {
+        for (size_t q = 0; q < na; q++) std::fprintf(stderr, "always[%zu] = sphere %u, r = %.3f\n", q, bvh.slot_to_sphere[q], sp[bvh.slot_to_sphere[q]].radius);
+        const std::vector<std::vector<int>> orders = {{0, 1, 2, 3}, {1, 2, 3, 0}};
+        for (const auto& ord : orders)
+            for (int far = 0; far < 2; far++) {
+                double seq = 0, pairs = 0, full = 0;
+                size_t waves = 0;
+                for (size_t w0 = 0; w0 + 64 <= rays.size(); w0 += 64, ++waves) {
+                    bool any[4] = {}, any01 = false, any23 = false, p01 = false, p23 = false;
+                    int mx = 0;
+                    for (int l = 0; l < 64; l++) {
+                        const Ray& R = rays[w0 + l];
+                        double closest = INFINITY;
+                        bool v[4];
+                        for (int i = 0; i < 4; i++) {
+                            const rt_sphere& S = sp[bvh.slot_to_sphere[ord[i]]];
+                            const int c = cand_class(S, R.o, R.d, 1e-3, closest);
+                            v[i] = far ? c == 2 : c >= 1;
+                            closest = std::min(closest, hit_sphere(S, R.o, R.d, 1e-3, closest));
+                        }
+                        for (int i = 0; i < 4; i++) any[i] |= v[i];
+                        any01 |= v[0] || v[1]; p01 |= v[0] && v[1];
+                        any23 |= v[2] || v[3]; p23 |= v[2] && v[3];
+                        mx = std::max(mx, (int)v[0] + v[1] + v[2] + v[3]);
+                    }
+                    seq += any[0] + any[1] + any[2] + any[3];
+                    pairs += any01 + p01 + any23 + p23;
+                    full += mx;
+                }
+                std::fprintf(stderr, "always-list blocks per wave, order %d%d%d%d%s: seq %.3f, pairs %.3f, full %.3f\n",
+                             ord[0], ord[1], ord[2], ord[3], far ? " + far filter" : "", seq / waves, pairs / waves, full / waves);
+            }
+    }
     if (sim_far)
         std::fprintf(stderr, "far filter (lockstep waves of 64 rays): candidate blocks per wave: always-list %.3f -> %.3f, "
                      "leaf rounds %.3f -> %.3f\n", al_blocks_now / nw, al_blocks_far / nw, lf_blocks_now / nw, lf_blocks_far / nw);
