@@ -1325,17 +1325,22 @@ int rt_render(const rt_camera* cam, const rt_sphere* spheres, size_t n, const rt
     for (rt_context* c : g_cache) scene_cached = scene_cached || (c && same_spheres(c->scene, spheres, n));
     SceneData pre;
     double prep_ms = 0;
+    bool prep_ok = false;  // the host thread finished (an exception there leaves it false)
     std::thread prep;
     bool pre_ready = false;
     {
         const uint32_t H0 = cam->image_height;
         const int G0 = opts && opts->n_gpus > 0 ? std::min<int>(opts->n_gpus, (int)H0) : 1;  // rows of the first device
         const uint64_t samples = (uint64_t)((H0 + (uint32_t)G0 - 1) / (uint32_t)G0) * cam->image_width * cam->samples_per_pixel;
-        auto job = [&pre, &prep_ms, spheres, n, cam, samples]() {
-            const auto t0 = std::chrono::steady_clock::now();
-            build_scene(spheres, n, pre);
-            prepare_tree(pre, *cam, samples);
-            prep_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        auto job = [&pre, &prep_ms, &prep_ok, spheres, n, cam, samples]() {
+            try {  // an exception must not leave the thread (std::terminate): the scene is rebuilt inline
+                const auto t0 = std::chrono::steady_clock::now();
+                build_scene(spheres, n, pre);
+                prepare_tree(pre, *cam, samples);
+                prep_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+                prep_ok = true;
+            } catch (...) {
+            }
         };
         if (!scene_cached) {
             try {
@@ -1350,7 +1355,9 @@ int rt_render(const rt_camera* cam, const rt_sphere* spheres, size_t n, const rt
             if (prep.joinable()) {
                 prep.join();
                 trace_note("host_scene_and_tree_thread", prep_ms);
-            } else {
+            }
+            if (!prep_ok) {  // no thread, or it failed: the records here, the tree in render_rows
+                pre = SceneData{};
                 build_scene(spheres, n, pre);
             }
             pre_ready = true;
