@@ -128,6 +128,39 @@ def dropin(cam, device):
     return times
 
 
+def all_devices_check(ndev, timeout=240):
+    """The drop-in over every GPU of the node, as the Zig shim calls it: tools/rt_render_c (a child
+    process; rt_scene_final -> rt_camera_build -> rt_render(n_gpus = 0) -> rt_ppm_save_p6) on the
+    reference's golden configuration (400x225, 10 spp, seed 0xdeadbeef: main.zig:41-55), once over
+    all visible devices and once on device 0 alone (RTZIG_DEVICE_MAP=0).  The RNG is keyed by the
+    global pixel, so the two P6 files must be identical (the multi-device branch is
+    otherwise rehearsed with logical devices on one GPU).  Runs after the timed region and the
+    process group, so a failure is reported here and never touches `value`."""
+    exe = os.path.join(ROOT, "raytracing-with-zig_amd", "rt_render_c")
+    cfg = ["400", "10", "0xdeadbeef", repr(16 / 9), "final"]
+    res = {"devices": ndev, "harness": "tools/rt_render_c (n_gpus = 0, RGB8, P6), golden config 400x225 10 spp"}
+    files = []
+    try:
+        with tempfile.TemporaryDirectory() as d:
+            for tag, extra in (("all", None), ("one", "0")):
+                path = os.path.join(d, tag + ".ppm")
+                env = {k: v for k, v in os.environ.items() if k != "RTZIG_DEVICE_MAP"}
+                if extra is not None:
+                    env["RTZIG_DEVICE_MAP"] = extra
+                t0 = time.perf_counter()
+                p = subprocess.run([exe, path] + cfg, env=env, capture_output=True, text=True, timeout=timeout)
+                res[tag + "_ms"] = round((time.perf_counter() - t0) * 1e3, 1)
+                if p.returncode:
+                    res["error"] = f"{tag}: exit {p.returncode}: {p.stderr.strip()[-300:]}"
+                    return res
+                files.append(open(path, "rb").read())
+    except (OSError, subprocess.SubprocessError) as e:
+        res["error"] = f"{type(e).__name__}: {e}"
+        return res
+    res["identical"] = files[0] == files[1]
+    return res
+
+
 def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -157,6 +190,8 @@ def parse_args(argv=None):
                          "(rt_render_rows_async_split); 'deferred' also leaves a direct-mode frame's reduce "
                          "pass to the next frame's drained waves (rt_render_rows_async_deferred), gathering "
                          "each frame once the next one is issued")
+    ap.add_argument("--no-device-check", action="store_true",
+                    help="at N > 1, skip rank 0's rt_render(n_gpus = 0) check over every visible GPU")
     ap.add_argument("--launch-check", action="store_true",
                     help="start the ranks and join the process group, print one line, render nothing")
     return ap.parse_args(argv)
@@ -463,6 +498,13 @@ def run(args):
     renderer.sync()
     renderer.close()
 
+    if grouped:
+        dist.destroy_process_group()
+    # N > 1 on a multi-GPU node: the drop-in's own multi-device branch over every visible GPU
+    # (rank 0 only, after the other ranks are done with their devices' work)
+    device_check = None
+    if rank == 0 and world > 1 and not args.no_device_check:
+        device_check = all_devices_check(ndev) if ndev > 1 else {"devices": ndev, "skipped": "one visible device"}
     if rank == 0:
         total_samples = W * H * spp * args.steps
         value = total_samples / elapsed_max / 1e6
@@ -585,6 +627,7 @@ def run(args):
             "cpu_baseline": None,
             "fast_f32": fast,
             **({"check": "gathered frame == whole-image render, bit for bit"} if check else {}),
+            **({"rt_render_all_devices": device_check} if device_check is not None else {}),
         }
         if world == 1 and not args.no_dropin and n_rows:
             times = dropin(cam, local_dev)
@@ -597,8 +640,6 @@ def run(args):
             res["cpu_baseline"] = cpu_baseline(W, args.aspect, args.cpu_spp)
             res["speedup_vs_cpu_baseline"] = round(value / res["cpu_baseline"]["value"], 1)
         print(json.dumps(res), flush=True)
-    if grouped:
-        dist.destroy_process_group()
 
 
 if __name__ == "__main__":

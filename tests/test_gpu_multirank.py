@@ -123,3 +123,16 @@ def test_bench_rccl_gather_world1_bit_exact():
     assert line["n_gpus"] == 1
     assert "RCCL gather to rank 0 (1-rank group" in line["config"]["parallelism"]
     assert line["check"].startswith("gathered frame == whole-image render")
+
+
+def test_bench_all_devices_check():
+    """bench.py's post-run drop-in check (rank 0 at N > 1): tools/rt_render_c with rt_render(n_gpus
+    = 0) over every visible GPU against the same call on device 0 alone — identical P6 files
+    (camera.zig:123-145 through the C ABI; on a 1-GPU box both calls use the one device)."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    import bench
+    import torch
+    res = bench.all_devices_check(torch.cuda.device_count())
+    assert res.get("identical") is True, res
