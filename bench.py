@@ -498,6 +498,7 @@ def run(args):
     renderer.sync()
     renderer.close()
 
+    group_size = dist.get_world_size() if grouped else 1
     if grouped:
         dist.destroy_process_group()
     # N > 1 on a multi-GPU node: the drop-in's own multi-device branch over every visible GPU
@@ -543,7 +544,7 @@ def run(args):
             "metric": METRIC,
             "value": round(value, 3),
             "unit": "Msamples/s",
-            "n_gpus": dist.get_world_size() if grouped else 1,
+            "n_gpus": group_size,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(frame_ms, 3),
