@@ -87,15 +87,18 @@ constexpr const char* kStallMsg =
 // previous mark to its phase.  Marks are taken only on the thread that called rt_render (the
 // per-device threads of a multi-GPU call are covered by the mark after they join).
 struct PhaseTrace {
-    std::thread::id tid;
     std::chrono::steady_clock::time_point t0, last;
     std::vector<std::pair<std::string, double>> ms;
 };
-PhaseTrace g_trace;                    // written only under g_cache_mu by the tracing rt_render call
-std::atomic<bool> g_trace_on{false};   // read by every mark (context calls of other threads too)
+PhaseTrace g_trace;  // touched only by the tracing thread (g_trace_tid), under g_cache_mu
+// the thread of the rt_render call being traced (default id: none); every mark reads it, on any
+// thread (context calls of other threads too), so it is the one shared word
+std::atomic<std::thread::id> g_trace_tid{};
+
+bool tracing() { return g_trace_tid.load(std::memory_order_relaxed) == std::this_thread::get_id(); }
 
 void trace_mark(const char* phase) {
-    if (!g_trace_on.load(std::memory_order_relaxed) || std::this_thread::get_id() != g_trace.tid) return;
+    if (!tracing()) return;
     const auto now = std::chrono::steady_clock::now();
     const double d = std::chrono::duration<double, std::milli>(now - g_trace.last).count();
     g_trace.last = now;
@@ -109,7 +112,7 @@ void trace_mark(const char* phase) {
 
 // a duration measured elsewhere (a host thread), reported under its own name
 void trace_note(const char* name, double ms) {
-    if (!g_trace_on.load(std::memory_order_relaxed) || std::this_thread::get_id() != g_trace.tid) return;
+    if (!tracing()) return;
     g_trace.ms.emplace_back(std::string("[") + name + "]", ms);
 }
 
@@ -1202,12 +1205,11 @@ struct TraceScope {
         const char* e = std::getenv("RTZIG_TRACE");
         if (!(e && *e && std::strcmp(e, "0") != 0)) return;
         g_trace = PhaseTrace{};
-        g_trace.tid = std::this_thread::get_id();
         g_trace.t0 = g_trace.last = std::chrono::steady_clock::now();
-        g_trace_on = true;
+        g_trace_tid.store(std::this_thread::get_id(), std::memory_order_relaxed);
     }
     ~TraceScope() {
-        if (!g_trace_on) return;
+        if (!tracing()) return;
         trace_mark("return");
         const double total = std::chrono::duration<double, std::milli>(g_trace.last - g_trace.t0).count();
         std::string j = "{\"rt_render_trace\": {\"total_ms\": " + std::to_string(total) + ", \"phases_ms\": {";
@@ -1217,7 +1219,7 @@ struct TraceScope {
         for (size_t i = 0; i < kernel_ms.size(); i++) j += (i ? ", " : "") + std::to_string(kernel_ms[i]);
         j += "]}}\n";
         std::fputs(j.c_str(), stderr);
-        g_trace_on = false;
+        g_trace_tid.store(std::thread::id{}, std::memory_order_relaxed);
     }
 };
 
@@ -1388,7 +1390,7 @@ int rt_render(const rt_camera* cam, const rt_sphere* spheres, size_t n, const rt
     std::vector<rt_context*> ctxs;
     rc = cached_contexts(map, first, G, spheres, n, scene, ctxs);
     if (rc) return rc;
-    if (g_trace_on)
+    if (tracing())
         for (rt_context* c : ctxs) (void)rt_context_enable_timing(c, 1);
     std::vector<uint32_t> rows(G);
     for (int g = 0; g < G; g++) {
@@ -1472,7 +1474,7 @@ int rt_render(const rt_camera* cam, const rt_sphere* spheres, size_t n, const rt
         for (auto& t : th) t.join();
         trace_mark("device_wait_and_uninterleave_threads");
     }
-    if (g_trace_on)
+    if (tracing())
         for (rt_context* c : ctxs) {
             double k = 0;
             if (rt_context_kernel_times(c, &k, nullptr) == RT_OK) trace.kernel_ms.push_back(k);

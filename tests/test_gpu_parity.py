@@ -281,6 +281,35 @@ def test_c_harness_end_to_end(oracle, golden_dir, tmp_path, device_map):
     _check_vs_chapter14(oracle, rgb, golden_dir)
 
 
+def test_c_harness_phase_trace(tmp_path):
+    """RTZIG_TRACE=1 (the one-shot cost breakdown of profiles/r05_dropin/): the harness's rt_render
+    prints one JSON line of phases — HIP init first, the return last, the host scene/tree thread as a
+    note — with one sample-kernel time per logical device, and its P6 file equals the untraced one."""
+    import json
+    import subprocess
+    exe = os.path.join(os.path.dirname(rtzig.LIB_PATH), "rt_render_c")
+    files = []
+    for trace in ("0", "1"):
+        out = str(tmp_path / f"t{trace}.ppm")
+        env = dict(os.environ, RTZIG_DEVICE_MAP="0,0,0", RTZIG_TRACE=trace)
+        p = subprocess.run([exe, out, "400", "10", "0xdeadbeef"], check=True, capture_output=True, text=True,
+                           timeout=300, env=env)
+        files.append(open(out, "rb").read())
+        lines = [json.loads(ln) for ln in p.stderr.splitlines() if ln.startswith('{"rt_render_trace"')]
+        if trace == "0":
+            assert not lines
+            continue
+        assert len(lines) == 1, p.stderr[-2000:]
+        t = lines[0]["rt_render_trace"]
+        phases = list(t["phases_ms"])
+        assert phases[0] == "hip_init_device_map" and phases[-1] == "return", phases
+        assert "[host_scene_and_tree_thread]" in phases
+        assert len(t["kernel_ms"]) == 3 and all(k > 0 for k in t["kernel_ms"])
+        timed = sum(v for k, v in t["phases_ms"].items() if not k.startswith("["))
+        assert abs(timed - t["total_ms"]) <= 0.01 * t["total_ms"] + 0.1
+    assert files[0] == files[1]
+
+
 @pytest.mark.parametrize("mode", ["ring", "direct"])
 @pytest.mark.parametrize("variant", ["bvh", "smem_u4", "lds_u4"])
 def test_walk_variants_bit_exact(oracle, variant, mode, monkeypatch):
