@@ -67,6 +67,27 @@ _VREG = re.compile(r"\bv\[?(\d+)(?::(\d+))?\]?")
 _SREG = re.compile(r"(?<![\w])(s\[?\d+|vcc|exec|m0|ttmp)")
 
 
+def fast_penalty(ins, table):
+    """Why a fast-form opcode issues at the slow rate: "sgpr" (an SGPR source), "3vgpr" (a third
+    distinct VGPR source), or None (not a fast-form opcode, or issued fast)."""
+    parts = ins.split(None, 1)
+    op = re.sub(r"_(e32|e64|sdwa|dpp)$", "", parts[0])
+    if op not in table["fast_rule"]["opcodes"]:
+        return None
+    ops = [o.strip() for o in (parts[1] if len(parts) > 1 else "").split(",")]
+    srcs = ops[1:] if not op.startswith("v_fmac") else ops
+    if op.startswith("v_add_co") or op.startswith("v_sub_co"):
+        srcs = ops[2:]
+    vregs, sgpr = set(), False
+    for s in srcs:
+        s = s.split()[0] if s else s
+        if s.startswith("v") and not s.startswith("vcc"):
+            vregs.add(s.lstrip("-|"))
+        elif re.match(r"^-?\|?(s\[|s\d|vcc|exec|m0|ttmp)", s):
+            sgpr = True
+    return "sgpr" if sgpr else ("3vgpr" if len(vregs) > 2 else None)
+
+
 def price(ins, table):
     """Issue cost of one assembly instruction (opcode + operands) under the table's model."""
     parts = ins.split(None, 1)

@@ -224,6 +224,7 @@ def main():
     opcnt = collections.Counter()  # executions per opcode
     regop = collections.Counter()  # issue cycles per (region, opcode)
     unpriced = collections.Counter()
+    pen = collections.Counter()    # cycles fast-form ops lose to an SGPR or third VGPR source
     for k, r, ins in per:
         c = klass(ins)
         static[r][c] += 1
@@ -264,6 +265,9 @@ def main():
             opcyc[op] += w * rt
             opcnt[op] += w
             regop[(r, op)] += w * rt
+            why = issue_rates.fast_penalty(ins, table)
+            if why and r not in ("rare", "prologue", "epilogue", "?"):
+                pen[(r, op, why)] += w * (rt - table["fast_rule"]["fast"])
             if r not in ("rare", "prologue", "epilogue", "?") and not re.match(
                     r"^v_(add|mul|fma|fmac)_f64|^v_(rsq|rcp|sqrt|exp|log|sin|cos)_f(32|64)", op):
                 other["n"] += w
@@ -297,7 +301,10 @@ def main():
                                            for o, c in opcyc.most_common(25)],
            "top_region_opcodes": [{"region": k[0], "op": k[1], "share": round(c / tcyc, 4)}
                                   for k, c in regop.most_common(40)],
-           "unpriced_opcodes (sibling rate used)": {o: c for o, c in unpriced.most_common(10)}}
+           "unpriced_opcodes (sibling rate used)": {o: c for o, c in unpriced.most_common(10)},
+           "fast_form_penalty": {"total_share": round(sum(pen.values()) / tcyc, 4) if tcyc else None,
+                                 "top": [{"region": k[0], "op": k[1], "why": k[2], "share": round(c / tcyc, 4)}
+                                         for k, c in pen.most_common(20)]}}
     try:
         pm = json.load(open(args.pmc))["counters_per_frame"]
         res["pmc"] = {"valu": pm["SQ_INSTS_VALU"], "salu": pm["SQ_INSTS_SALU"], "lds": pm["SQ_INSTS_LDS"],
