@@ -402,6 +402,11 @@ constexpr int kRefetchK = RTZIG_REFETCH_K;
 #ifndef RTZIG_DRAIN
 #define RTZIG_DRAIN 0
 #endif
+// Waves per block that start the deferred fold before tracing (path_loop; 0: only drained waves fold)
+#ifndef RTZIG_FOLD_HEAD
+#define RTZIG_FOLD_HEAD 1
+#endif
+constexpr int kFoldHead = RTZIG_FOLD_HEAD;  // (1 measured best: 2 / 4, or 1 in every 2nd / 4th block, fold slower)
 constexpr bool kDrainMode = RTZIG_DRAIN != 0;     // drained walks do not suspend
 constexpr bool kDrainTrips = RTZIG_DRAIN == 1;    // drained trips are not capped (RTZIG_DRAIN=2: walks only)
 #ifndef RTZIG_REFILL_MIN
@@ -1240,6 +1245,14 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
     uint32_t n_iter = 0, n_trip = 0, n_seed = 0, n_wstart = 0, n_shade = 0, n_fin = 0;
     uint64_t rt_start = 0, rt_drain = 0;  // s_memrealtime (100 MHz) at start / first empty claim (kProf only)
     if constexpr (kProf) rt_start = __builtin_amdgcn_s_memrealtime();
+
+    // Head fold: the previous deferred call's reduce pass (rt_render_rows_async_deferred) is started
+    // by the first kFoldHead waves of every block before they trace, while the block's other waves
+    // trace; the drained waves at the end take what is left (below).  Left to the drained waves
+    // alone, most of it waited for waves to finish their last long paths and ran after the tail.
+    if constexpr (kDirect && !kProf) {
+        if (kFoldHead > 0 && ua.fold.samples != nullptr && threadIdx.x / 64 < (uint32_t)kFoldHead) fold_chunks(ua.fold, lane);
+    }
 
     while (true) {
         uint64_t t_top = 0;
