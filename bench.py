@@ -190,6 +190,8 @@ def parse_args(argv=None):
                          "(rt_render_rows_async_split); 'deferred' also leaves a direct-mode frame's reduce "
                          "pass to the next frame's drained waves (rt_render_rows_async_deferred), gathering "
                          "each frame once the next one is issued")
+    ap.add_argument("--row-buffers", type=int, default=3, choices=[2, 3, 4],
+                    help="N > 1: row buffers the frame loop rotates through (gather overlap)")
     ap.add_argument("--no-device-check", action="store_true",
                     help="at N > 1, skip rank 0's rt_render(n_gpus = 0) check over every visible GPU")
     ap.add_argument("--launch-check", action="store_true",
@@ -281,18 +283,21 @@ def run(args):
     renderer = rtzig.DeviceRenderer(local_dev)
     renderer.set_scene(cam.scene.world)
     renderer.enable_timing(True)
-    # Two row buffers and a render stream of their own: frame k renders into outs[k % 2] on `stream`
-    # while the collective stream (the current one, which RCCL's gather joins) still gathers frame
-    # k - 1 from the other buffer — the gather overlaps the next frame's render instead of adding to
-    # it.  A buffer is rendered into again only after its previous gather has finished (`freed`).
+    # Row buffers (--row-buffers, 3) and a render stream of their own: frame k renders into
+    # outs[k % NB] on `stream` while the collective stream (the current one, which RCCL's gather
+    # joins) still gathers earlier frames from the others — the gather overlaps the next frame's
+    # render instead of adding to it.  A buffer is rendered into again only after its previous gather
+    # has finished (`freed`); with three, that gather is two frames old, so a deferred frame's kernel
+    # does not wait for the previous kernel's completion to travel through the collective stream.
     dt = torch.float64 if args.output == "linear" else torch.uint8
-    outs = [torch.zeros((R, W, 3), dtype=dt, device=dev) for _ in range(2)]
+    NB = args.row_buffers
+    outs = [torch.zeros((R, W, 3), dtype=dt, device=dev) for _ in range(NB)]
     out = outs[0]
     stats = torch.zeros(2, dtype=torch.int64, device=dev)
     coll = torch.cuda.current_stream()
     stream = torch.cuda.Stream(device=dev) if grouped else coll
-    rendered = [torch.cuda.Event() for _ in range(2)]
-    freed = [None, None]
+    rendered = [torch.cuda.Event() for _ in range(NB)]
+    freed = [None] * NB
     nframe = [0]
     torch.cuda.synchronize()
     init_ms = (time.perf_counter() - t_init) * 1e3
@@ -311,7 +316,7 @@ def run(args):
         # frame (nothing pending) is gathered at once, as with the split call
         j = nframe[0]
         nframe[0] += 1
-        b, pb = j % 2, (j - 1) % 2
+        b, pb = j % NB, (j - 1) % NB
         # the kernel writes its own rows into outs[b] (a call that cannot fold the pending pass runs it
         # first and writes outs[b] directly), and with a pass pending it also folds into outs[pb]: both
         # buffers' last gathers must have finished (in steady state both events have long completed)
@@ -344,7 +349,7 @@ def run(args):
             return None
         renderer.flush()
         pend[0] = False
-        b = (nframe[0] - 1) % 2
+        b = (nframe[0] - 1) % NB
         img = gather(outs[b])
         freed[b] = torch.cuda.Event()
         freed[b].record(coll)
@@ -353,7 +358,7 @@ def run(args):
     def frame(stats_ptr=None):
         if stream is not coll and args.pipeline == "deferred":
             return frame_deferred(stats_ptr)
-        b = nframe[0] % 2
+        b = nframe[0] % NB
         nframe[0] += 1
         buf = outs[b]
         if freed[b] is not None:

@@ -1018,9 +1018,16 @@ int render_rows(rt_context* ctx, const rt_camera* cam, uint32_t output_format, u
     }
     if (ev) HIP_CHECK(hipEventRecord(ev[2], rs));
     if (folding) {
-        // the chunks of the previous deferred call that no drained wave took
-        HIP_CHECK(rtk_launch_fold_rest(&ctx->fold, rs));
-        HIP_CHECK(hipEventRecord(ctx->reduced[ctx->fold_buf], rs));
+        if (p.prof) {
+            // the instrumented kernels do not fold: the pass runs whole after them
+            HIP_CHECK(rtk_launch_fold_rest(&ctx->fold, rs));
+            HIP_CHECK(hipEventRecord(ctx->reduced[ctx->fold_buf], rs));
+        } else {
+            // every wave of the launch claims fold chunks until none is left before it exits
+            // (path_loop), so the pass is complete with the kernel: no follow-up pass, and the next
+            // launch on this stream finds the buffer free without waiting on the output stream
+            HIP_CHECK(hipEventRecord(ctx->reduced[ctx->fold_buf], s));
+        }
         ctx->reduced_valid[ctx->fold_buf] = true;
         ctx->fold_pending = false;
     }

@@ -707,9 +707,11 @@ def test_split_render_pipeline_bit_exact(oracle, mode, monkeypatch):
 
 
 @pytest.mark.parametrize("mode", ["direct", "ring"])
-def test_deferred_render_pipeline_bit_exact(oracle, mode, monkeypatch):
+@pytest.mark.parametrize("profile", [False, True])
+def test_deferred_render_pipeline_bit_exact(oracle, mode, profile, monkeypatch):
     """rt_render_rows_async_deferred: a direct-mode call's reduce pass is left pending and folded by
-    the next deferred call's drained waves (plus a follow-up pass for the chunks they left); the last
+    the next deferred call's waves (one wave per block first, then the drained waves; the
+    instrumented kernels do not fold, so a follow-up pass runs it after them: `profile`); the last
     one by rt_context_flush.  Five frames into two row buffers, each taken on the second stream once
     it is complete (after the next call, or after the flush), interleaved with a plain call that must
     run the pending pass first: every frame bit-exact against oracle B, exact sample counts (reference:
@@ -720,9 +722,10 @@ def test_deferred_render_pipeline_bit_exact(oracle, mode, monkeypatch):
     ref, rays = oracle.render_b(cam.cam, cam.scene.world, row0=5, row_step=8, n_rows=12, threads=16)
     r = rtzig.DeviceRenderer(0)
     r.set_scene(cam.scene.world)
+    r.enable_profile(profile)
     render, coll = torch.cuda.Stream(), torch.cuda.Stream()
     outs = [torch.zeros((12, 1200, 3), dtype=torch.float64, device="cuda:0") for _ in range(2)]
-    stats = torch.zeros(2, dtype=torch.int64, device="cuda:0")
+    stats = torch.zeros(rtzig.abi.RT_PROFILE_STATS_WORDS, dtype=torch.int64, device="cuda:0")
     got = []
     pending = False
     for k in range(5):

@@ -43,6 +43,7 @@ ap.add_argument("--pipe-frames", type=int, default=0,
                 help="also time each rank's rows in bench.py's frame pipeline (two row buffers, render "
                      "stream, output completed on a second stream: rt_render_rows_async_split), this many "
                      "frames, wall clock per frame")
+ap.add_argument("--row-buffers", type=int, default=3, help="row buffers the pipeline rotates through (bench.py)")
 ap.add_argument("--pipe-mode", choices=["plain", "split", "deferred"], default="deferred",
                 help="the pipeline's render call (bench.py --pipeline)")
 args = ap.parse_args()
@@ -65,18 +66,19 @@ def kernel_ms(row0, step, n_rows):
 
 
 def pipeline_ms(row0, step, n_rows):
-    """bench.py's N > 1 loop without the collective: frame k renders into buffer k % 2 on the render
+    """bench.py's N > 1 loop without the collective: frame k renders into buffer k % NB on the render
     stream with its output completed on the second stream, where the gather would run (split: the
     reduce pass there; deferred: folded by the next frame's drained waves, the last one flushed);
     wall clock per frame over args.pipe_frames frames."""
     render, coll = torch.cuda.Stream(), torch.cuda.Stream()
-    outs = [torch.empty((n_rows, W, 3), dtype=torch.float64, device="cuda:0") for _ in range(2)]
-    freed = [None, None]
+    NB = args.row_buffers
+    outs = [torch.empty((n_rows, W, 3), dtype=torch.float64, device="cuda:0") for _ in range(NB)]
+    freed = [None] * NB
     pend = [False]
     deferred = args.pipe_mode == "deferred"
 
     def frame(k):
-        b, pb = k % 2, (k - 1) % 2
+        b, pb = k % NB, (k - 1) % NB
         # the kernel writes its own rows (outs[b]) and, with a pass pending, folds into outs[pb]
         for wb in ((b, pb) if pend[0] else (b,)):
             if freed[wb] is not None:
@@ -111,7 +113,7 @@ def pipeline_ms(row0, step, n_rows):
     torch.cuda.synchronize()
     best = None
     for _ in range(args.reps):
-        freed[0] = freed[1] = None
+        freed[:] = [None] * NB
         t0 = time.perf_counter()
         for k in range(args.pipe_frames):
             frame(k)
@@ -120,23 +122,35 @@ def pipeline_ms(row0, step, n_rows):
         ms = (time.perf_counter() - t0) / args.pipe_frames * 1e3
         best = ms if best is None else min(best, ms)
     ws[0] = max(ws[0], r.workspace_bytes())
+    # one more pass with HIP-event timing: the sample kernel (with the fold inside, deferred) and the
+    # reduce / follow-up passes per frame, to split the frame into kernel time and what lies between
+    r.enable_timing(True)
+    freed[:] = [None] * NB
+    for k in range(args.pipe_frames):
+        frame(k)
+    finish()
+    torch.cuda.synchronize()
+    s_ms, r_ms, _ = r.kernel_times_total()
+    split[0] = (s_ms / args.pipe_frames, r_ms / args.pipe_frames)
     return best
 
 
 ws = [0]  # the largest workspace a rank's pipeline held (rt_context_workspace_bytes)
+split = [(0.0, 0.0)]  # the last pipeline's (sample kernel, reduce / follow-up pass) ms per frame
 res = {"config": f"{W}x{H} {args.spp}spp", "unit_mode_env": os.environ.get("RTZIG_UNIT_MODE"),
        "pipe_mode": args.pipe_mode if args.pipe_frames else None, "link_GBps_model": LINK_GBPS, "launch_us_model": LAUNCH_US, "ranks": {}}
 base = None
 pipe_base = None
 for n in args.ns:
     R = rdist.rows_per_rank(H, n)
-    per_rank, per_rank_pipe = [], []
+    per_rank, per_rank_pipe, per_rank_split = [], [], []
     ws[0] = 0
     for rank in range(n):
         row0, step, n_rows = rdist.rank_rows(H, rank, n)
         per_rank.append(kernel_ms(row0, step, n_rows))
         if args.pipe_frames:
             per_rank_pipe.append(pipeline_ms(row0, step, n_rows))
+            per_rank_split.append(split[0])
         print(f"N={n} rank {rank}: {per_rank[-1]:.3f} ms" +
               (f", pipelined {per_rank_pipe[-1]:.3f} ms per frame" if per_rank_pipe else ""), file=sys.stderr, flush=True)
     k = max(per_rank)
@@ -172,5 +186,8 @@ for n in args.ns:
         res["ranks"][n].update({"pipelined_frame_ms_max_over_ranks": round(max(per_rank_pipe), 3),
                                 "pipelined_frame_ms_min_over_ranks": round(min(per_rank_pipe), 3),
                                 "efficiency_pipelined": round(pipe_base / pf / n, 3),
-                                "workspace_GiB_max_over_ranks": round(ws[0] / 2**30, 3)})
+                                "workspace_GiB_max_over_ranks": round(ws[0] / 2**30, 3),
+                                # the slowest rank's frame split by HIP events (one more timed pass)
+                                "pipelined_sample_kernel_ms_slowest_rank": round(per_rank_split[per_rank_pipe.index(max(per_rank_pipe))][0], 3),
+                                "pipelined_reduce_ms_slowest_rank": round(per_rank_split[per_rank_pipe.index(max(per_rank_pipe))][1], 3)})
 print(json.dumps(res))
