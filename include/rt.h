@@ -168,8 +168,9 @@ int rt_render_rows_async_split(rt_context* ctx, const rt_camera* cam, uint32_t o
                                void* d_out, void* d_stats, void* stream, void* out_stream);
 /* Deferred variant for frame pipelines (bench.py's N > 1 loop): like the split call, but a
  * direct-mode call's reduce pass is left PENDING — the next deferred call's sample kernel folds it
- * with the waves that run out of items while a few long paths finish (the launch's tail, where the
- * CUs otherwise idle), and a short follow-up pass on that call's out_stream takes the chunks they left.
+ * (one wave per block starts on it before tracing; the waves that run out of items while a few long
+ * paths finish take the rest) and completes it before the kernel ends; with profiling enabled the
+ * instrumented kernel does not fold, and a pass on that call's out_stream runs it after the kernel.
  * So the output of call k is complete on ITS out_stream once call k+1 has been issued and its
  * out_stream reaches that point, or after rt_context_flush(ctx) / rt_context_sync(ctx), which run a
  * pending pass whole.  A call that cannot fold the pending pass (a plain or ring-mode call, another
