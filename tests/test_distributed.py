@@ -3,6 +3,7 @@ the final gather to rank 0.  Each rank renders its rows with a CPU stand-in (ora
 the product renders on the GPU); the gathered image must equal the single-rank image bit-for-bit."""
 import os
 import socket
+import sys
 
 import numpy as np
 import pytest
@@ -146,3 +147,30 @@ def test_bench_collective_flag_forms_one_rank_group():
     rc, lines, err = _bench(["--gpus", "1", "--collective", "--launch-check"])
     assert rc == 0, err[-2000:]
     assert lines == [{"launch_check": True, "n_gpus": 1, "gpus_arg": 1}]
+
+
+def test_bench_pipeline_options_parse():
+    """bench.py's N > 1 loop options: the deferred pipeline over three row buffers by default;
+    plain / split and 2-4 row buffers selectable; anything else refused."""
+    import importlib
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    bench = importlib.import_module("bench")
+    a = bench.parse_args([])
+    assert a.pipeline == "deferred" and a.row_buffers == 3 and not a.no_device_check
+    a = bench.parse_args(["--pipeline", "plain", "--row-buffers", "2", "--no-device-check"])
+    assert a.pipeline == "plain" and a.row_buffers == 2 and a.no_device_check
+    for bad in (["--row-buffers", "1"], ["--pipeline", "fused"]):
+        with pytest.raises(SystemExit):
+            bench.parse_args(bad)
+
+
+def test_bench_device_check_reports_instead_of_raising(tmp_path, monkeypatch):
+    """The post-run all-devices check (rank 0 at N > 1) turns any harness failure into an `error`
+    field of the JSON line — it never raises, so the bench line is printed whatever happens
+    (here: a harness that does not exist)."""
+    import importlib
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    bench = importlib.import_module("bench")
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+    res = bench.all_devices_check(8, timeout=30)
+    assert res["devices"] == 8 and "error" in res and "identical" not in res
