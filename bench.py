@@ -181,7 +181,7 @@ def parse_args(argv=None):
                          "a whole-image render on its own device (tests: the pipelined gather path)")
     ap.add_argument("--collective", action="store_true",
                     help="at --gpus 1, still join a (1-rank) process group on --dist-backend and run the "
-                         "N>1 pipeline: two row buffers, the render stream, and each frame's dist.gather on "
+                         "N>1 pipeline: the row buffers, the render stream, and each frame's dist.gather on "
                          "the collective stream (nccl: the RCCL gather on one GPU)")
     ap.add_argument("--pipeline", choices=["plain", "split", "deferred"], default="deferred",
                     help="N > 1 frame loop: 'plain' completes each frame on the render stream (one "
@@ -263,7 +263,7 @@ def run(args):
     torch.cuda.set_device(local_dev)
     dev = torch.device("cuda", local_dev)
     # grouped: a process group exists (N > 1, or --collective at N = 1); the pipeline below (render
-    # stream + collective stream, two row buffers, dist.gather per frame) runs whenever it does
+    # stream + collective stream, --row-buffers row buffers, dist.gather per frame) runs whenever it does
     grouped = world > 1 or args.collective
     if grouped and world == 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -442,7 +442,7 @@ def run(args):
     renderer.sync()  # raises if a wave of any timed frame gave up on a hand-off (sticky error word)
     check = None
     if args.check and rank == 0 and n_rows:
-        # the last timed frame as gathered (two row buffers, gather overlapped with the next render)
+        # the last timed frame as gathered (row buffers in rotation, gather overlapped with the next render)
         # against one whole-image render on this device: the RNG is keyed by the global pixel, so
         # they must agree bit for bit
         whole = torch.empty((H, W, 3), dtype=dt, device=dev)
@@ -565,14 +565,14 @@ def run(args):
                            + ((", RCCL gather to rank 0" if args.dist_backend == "nccl" else
                                ", gloo gather to rank 0 (rehearsal: ranks share devices)")
                               + (" (1-rank group, --collective)" if world == 1 else "")
-                              + (", each frame's gather overlapped with the next frame's render (two row buffers); "
-                                 "a direct-mode frame's reduce pass folded by the next frame's drained waves "
+                              + (f", each frame's gather overlapped with the next frame's render ({NB} row buffers); "
+                                 "a direct-mode frame's reduce pass folded inside the next frame's sample kernel "
                                  "(rt_render_rows_async_deferred)" if args.pipeline == "deferred" else
-                                 ", each frame's gather overlapped with the next frame's render (two row buffers); "
+                                 f", each frame's gather overlapped with the next frame's render ({NB} row buffers); "
                                  "a direct-mode reduce pass on the render stream (one per-sample buffer)"
                                  if args.pipeline == "plain" else
                                  ", each frame's gather and a direct-mode reduce pass on the collective stream, "
-                                 "overlapped with the next frame's render (two row buffers; "
+                                 f"overlapped with the next frame's render ({NB} row buffers; "
                                  "rt_render_rows_async_split)")
                               if grouped else "")},
             "roofline": {
