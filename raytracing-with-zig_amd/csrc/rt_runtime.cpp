@@ -24,6 +24,7 @@
 #include <chrono>
 #include <exception>
 #include <functional>
+#include <future>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -402,10 +403,6 @@ bool needs_training(const SceneData& sd, const rt_camera& cam, uint64_t samples)
     return want_train(sd, samples) && !(sd.train_tried && same_view(sd.view, cam));
 }
 void train_bvh(SceneData& sd, const rt_camera& cam);
-void prepare_tree(SceneData& sd, const rt_camera& cam, uint64_t samples) {
-    if (needs_far_rebuild(sd, cam)) build_bvh(sd, far_bound(sd, cam));
-    if (needs_training(sd, cam, samples)) train_bvh(sd, cam);
-}
 
 void train_bvh(SceneData& sd, const rt_camera& cam) {
     static std::mutex mu;
@@ -460,11 +457,13 @@ bool same_spheres(const SceneData& sd, const rt_sphere* s, size_t n) {
 }
 
 // Runs a deferred call's pending reduce pass whole, on the stream its output was promised on, after
-// the last launch (which wrote or folded nothing of it since it is still pending).
-int flush_fold(rt_context* ctx) {
+// the last launch (which wrote or folded nothing of it since it is still pending).  own_stream: on
+// the context's own stream instead (rt_context_destroy, which waits for the pass before returning,
+// so the caller's stream — possibly destroyed already — is never touched there).
+int flush_fold(rt_context* ctx, bool own_stream = false) {
     if (!ctx->fold_pending) return RT_OK;
     ctx->fold_pending = false;
-    hipStream_t fs = ctx->fold_stream;
+    hipStream_t fs = own_stream ? ctx->stream : ctx->fold_stream;
     if (ctx->launched_valid) HIP_CHECK(hipStreamWaitEvent(fs, ctx->launched, 0));
     HIP_CHECK(hipMemsetAsync(ctx->fold.ctr, 0, sizeof(unsigned long long), fs));
     HIP_CHECK(rtk_launch_fold_rest(&ctx->fold, fs));
@@ -479,8 +478,8 @@ int flush_fold(rt_context* ctx) {
 // pending deferred reduce pass is run first.  `done` marks the end of the LAST call only: a reduce
 // pass of an earlier split / deferred call runs on that call's out stream and may still read its
 // per-sample buffer, so the passes' own events are waited for too.
-int quiesce(rt_context* ctx) {
-    int rc = flush_fold(ctx);
+int quiesce(rt_context* ctx, bool own_stream = false) {
+    int rc = flush_fold(ctx, own_stream);
     if (rc) return rc;
     if (ctx->done_valid) HIP_CHECK(hipEventSynchronize(ctx->done));
     for (int b = 0; b < 2; b++)
@@ -756,8 +755,12 @@ int rt_context_destroy(rt_context* ctx) {
     (void)hipSetDevice(ctx->device);
     // a deferred call's pending reduce pass is run, not dropped: its output was promised to the
     // caller (the reference's render always fills ppm.pixels, camera.zig:125,138); then every
-    // launch and pass that may still use a buffer is waited for before anything is freed
-    const int rc = quiesce(ctx);
+    // launch and pass that may still use a buffer is waited for before anything is freed.  The
+    // pass runs on the context's own stream (after the launch it depends on): destroy blocks until
+    // it is complete, so the caller's out stream gives no ordering the caller would not have anyway,
+    // and a caller may already have destroyed that stream.  A context whose stream was never
+    // created (a failed rt_context_create) has launched nothing and is not waited for.
+    const int rc = ctx->stream ? quiesce(ctx, true) : RT_OK;
     if (rc) {  // still free what can be freed after a device-wide wait
         (void)hipDeviceSynchronize();
     }
@@ -1337,15 +1340,33 @@ int rt_render(const rt_camera* cam, const rt_sphere* spheres, size_t n, const rt
     bool prep_ok = false;  // the host thread finished (an exception there leaves it false)
     std::thread prep;
     bool pre_ready = false;
+    // The training rule is per device launch (render_rows): the first device's rows.  With n_gpus = 0
+    // (every visible device) the device count is known only once the HIP runtime is up, so the
+    // thread builds the records and the SAH tree first and then waits for it (device_gpus below; 0:
+    // the call failed before, no training).
+    std::promise<int> gpus_promise;
+    std::shared_future<int> gpus = gpus_promise.get_future().share();
+    bool gpus_set = false;
+    auto device_gpus = [&](int g) {
+        if (!gpus_set) {
+            gpus_set = true;
+            gpus_promise.set_value(g);
+        }
+    };
     {
         const uint32_t H0 = cam->image_height;
-        const int G0 = opts && opts->n_gpus > 0 ? std::min<int>(opts->n_gpus, (int)H0) : 1;  // rows of the first device
-        const uint64_t samples = (uint64_t)((H0 + (uint32_t)G0 - 1) / (uint32_t)G0) * cam->image_width * cam->samples_per_pixel;
-        auto job = [&pre, &prep_ms, &prep_ok, spheres, n, cam, samples]() {
+        const int G_opt = opts && opts->n_gpus > 0 ? std::min<int>(opts->n_gpus, (int)H0) : 0;
+        auto job = [&pre, &prep_ms, &prep_ok, spheres, n, cam, H0, G_opt, gpus]() {
             try {  // an exception must not leave the thread (std::terminate): the scene is rebuilt inline
                 const auto t0 = std::chrono::steady_clock::now();
                 build_scene(spheres, n, pre);
-                prepare_tree(pre, *cam, samples);
+                if (needs_far_rebuild(pre, *cam)) build_bvh(pre, far_bound(pre, *cam));
+                const int G0 = G_opt > 0 ? G_opt : std::min<int>(gpus.get(), (int)H0);
+                if (G0 > 0) {
+                    const uint64_t samples =
+                        (uint64_t)((H0 + (uint32_t)G0 - 1) / (uint32_t)G0) * cam->image_width * cam->samples_per_pixel;
+                    if (needs_training(pre, *cam, samples)) train_bvh(pre, *cam);
+                }
                 prep_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
                 prep_ok = true;
             } catch (...) {
@@ -1373,12 +1394,14 @@ int rt_render(const rt_camera* cam, const rt_sphere* spheres, size_t n, const rt
         }
         return pre;
     };
-    struct Joiner {  // every return path joins the host thread
+    struct Joiner {  // every return path releases (no device count: no training) and joins the host thread
         std::thread& t;
+        std::function<void(int)> release;
         ~Joiner() {
+            release(0);
             if (t.joinable()) t.join();
         }
-    } joiner{prep};
+    } joiner{prep, device_gpus};
     std::vector<int> map;
     rc = device_map(map);  // the process's first HIP call initialises the runtime
     if (rc) return rc;
@@ -1392,6 +1415,7 @@ int rt_render(const rt_camera* cam, const rt_sphere* spheres, size_t n, const rt
     }
     const uint32_t W = cam->image_width, H = cam->image_height;
     G = std::min<int>(G, (int)H);
+    device_gpus(G);  // the host thread's training rule: the first device's ceil(H / G) rows
     const size_t px_bytes = o.output_format == RT_OUT_LINEAR_F64 ? 3 * sizeof(double) : 3;
 
     std::vector<rt_context*> ctxs;

@@ -128,11 +128,15 @@ def test_bench_rccl_gather_world1_bit_exact():
 def test_bench_all_devices_check():
     """bench.py's post-run drop-in check (rank 0 at N > 1): tools/rt_render_c with rt_render(n_gpus
     = 0) over every visible GPU against the same call on device 0 alone — identical P6 files
-    (camera.zig:123-145 through the C ABI; on a 1-GPU box both calls use the one device)."""
+    (camera.zig:123-145 through the C ABI).  Needs two physical GPUs: on one, both calls would use
+    the same device and the check would compare a render with itself (the logical-device form of
+    the multi-device branch is test_c_harness_end_to_end with RTZIG_DEVICE_MAP)."""
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path.insert(0, root)
     import bench
     import torch
+    if torch.cuda.device_count() < 2:
+        pytest.skip("needs >= 2 physical GPUs (one device would be compared with itself)")
     res = bench.all_devices_check(torch.cuda.device_count())
     assert res.get("identical") is True, res
