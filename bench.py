@@ -117,15 +117,46 @@ def pmc_summary(workload):
 
 
 def dropin(cam, device):
-    """The drop-in path's end-to-end cost: rt_render (n_gpus=1) of the same frame into host memory,
-    cold (first call of the process: context, scene + BVH upload, workspace, render, D2H) then warm
-    (cached context, same scene)."""
+    """The drop-in path's cost INSIDE this process: rt_render (n_gpus=1) of the same frame into host
+    memory, three calls.  The first creates rt_render's cached context (streams, scene + BVH upload,
+    workspace) in a process whose HIP runtime torch has already initialised — it is NOT a cold start
+    (dropin_one_shot is); the later calls reuse the cached context and scene."""
     times = []
     for _ in range(3):
         t0 = time.perf_counter()
         rtzig.render(cam.cam, cam.scene.world, n_gpus=1, device=device)
         times.append((time.perf_counter() - t0) * 1e3)
     return times
+
+
+def dropin_one_shot(width, spp, aspect, runs=3):
+    """The drop-in as the reference runs it — ONE image per process (main.zig:14-36): the C harness
+    of the Zig shim (tools/rt_render_c.c: rt_scene_final -> rt_camera_build -> rt_render(n_gpus = 0,
+    RGB8) -> rt_ppm_save_p6) started as a fresh child process per run, timed from spawn to the P6 file
+    written (tools/dropin_cold.py: the harness's CLOCK_MONOTONIC stamps and the library's phase
+    trace).  Everything a fresh process pays is inside: exec, library load, HIP runtime init, context,
+    scene + tree, the frame, the copy-out, the write."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import statistics
+    import dropin_cold
+    args = (str(width), str(spp), "0xdeadbeef", repr(aspect), "final")
+    res = {"harness": "tools/rt_render_c (fresh child process per run, n_gpus = 0, RGB8, P6)",
+           "args": {"width": width, "spp": spp, "aspect": aspect, "scene": "final"}}
+    try:
+        with tempfile.TemporaryDirectory() as d:
+            rs = [dropin_cold.one_run(args, os.path.join(d, f"{k}.ppm")) for k in range(runs)]
+    except (OSError, RuntimeError, subprocess.SubprocessError) as e:
+        res["error"] = f"{type(e).__name__}: {str(e)[-300:]}"
+        return res
+    med = lambda xs: round(statistics.median(xs), 2)  # noqa: E731
+    res.update({
+        "spawn_to_file_written_ms": [round(r["to_file_written_ms"], 2) for r in rs],
+        "median_spawn_to_file_written_ms": med([r["to_file_written_ms"] for r in rs]),
+        "median_spawn_to_exit_ms": med([r["total_ms"] for r in rs]),
+        "median_hip_runtime_init_ms": med([r["rt_render_phases_ms"].get("hip_init_device_map", 0.0) for r in rs]),
+        "median_frame_kernel_ms": med([r["kernel_ms"][0] for r in rs if r["kernel_ms"]]),
+    })
+    return res
 
 
 def all_devices_check(ndev, timeout=240):
@@ -637,11 +668,19 @@ def run(args):
         }
         if world == 1 and not args.no_dropin and n_rows:
             times = dropin(cam, local_dev)
-            res["dropin_ms"] = {"cold": round(times[0], 2), "warm": round(min(times[1:]), 2),
-                                "warm_over_frame": round(min(times[1:]) / frame_ms, 4),
-                                "note": "rt_render(n_gpus=1) into host memory (f64 linear): cold = first call of "
-                                        "the process (context, scene + BVH upload, workspace, render, D2H); "
-                                        "warm = cached context, same scene"}
+            one = dropin_one_shot(W, spp, args.aspect)
+            res["dropin_ms"] = {
+                "one_shot_process": one,
+                "one_shot_over_frame": (round(one["median_spawn_to_file_written_ms"] / frame_ms, 2)
+                                        if "median_spawn_to_file_written_ms" in one else None),
+                "first_call_hip_initialised": round(times[0], 2),
+                "warm": round(min(times[1:]), 2),
+                "warm_over_frame": round(min(times[1:]) / frame_ms, 4),
+                "note": "one_shot_process = a fresh process per image, spawn to the P6 file written (the "
+                        "reference's own use, main.zig:14-36); first_call_hip_initialised = the first "
+                        "rt_render(n_gpus=1) call inside this bench process, whose HIP runtime is already "
+                        "up (context, scene + BVH upload, workspace, render, D2H of f64 linear); warm = "
+                        "later calls on the cached context and scene"}
         if world == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(W, args.aspect, args.cpu_spp)
             res["speedup_vs_cpu_baseline"] = round(value / res["cpu_baseline"]["value"], 1)

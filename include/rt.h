@@ -194,6 +194,11 @@ int rt_context_sync(rt_context* ctx);
 int rt_context_set_precision(rt_context* ctx, int precision);
 /* Name of the kernel variant the context launches (for profiling / logs). */
 const char* rt_kernel_name(rt_context* ctx);
+/* The closest-hit structure the context's next render walks (diagnostics / tests), info[6]:
+ * {1 if the BVH walk runs (else the reference's list walk), tree nodes, leaves, depth, always-list
+ * spheres, 1 if the tree was trained on the rays of the last large launch's camera (DESIGN.md §5.4:
+ * same bits as any tree, fewer node visits)}. */
+int rt_context_tree_info(rt_context* ctx, uint32_t* info);
 /* Device bytes the context's render workspace holds now (rings, sums, flags, direct-mode samples,
  * schedule, counters; not the scene or caller buffers): see rt_render "Workspace". */
 int rt_context_workspace_bytes(rt_context* ctx, uint64_t* bytes);

@@ -1159,6 +1159,18 @@ int rt_context_kernel_times_total(rt_context* ctx, double* sample_ms, double* re
 
 const char* rt_kernel_name(rt_context* ctx) { return ctx ? ctx->last_kernel : "render_kernel"; }
 
+int rt_context_tree_info(rt_context* ctx, uint32_t* info) {
+    if (!ctx || !info) { rt_set_last_error("null context / output"); return RT_ERR_INVALID; }
+    const SceneData& sd = ctx->scene;
+    info[0] = ctx->n_spheres && use_bvh(ctx) ? 1u : 0u;
+    info[1] = sd.bvh_ok ? sd.n_nodes : 0u;
+    info[2] = sd.bvh_ok ? sd.n_leaves : 0u;
+    info[3] = sd.bvh_ok ? sd.depth : 0u;
+    info[4] = sd.bvh_ok ? sd.n_always : 0u;
+    info[5] = sd.bvh_ok && sd.trained ? 1u : 0u;
+    return RT_OK;
+}
+
 int rt_context_workspace_bytes(rt_context* ctx, uint64_t* bytes) {
     if (!ctx || !bytes) { rt_set_last_error("null context / output"); return RT_ERR_INVALID; }
     *bytes = (uint64_t)ctx->ring_bytes + ctx->sums_bytes + ctx->flags_bytes + ctx->samples_bytes + ctx->samples2_bytes +

@@ -239,6 +239,12 @@ class DeviceRenderer:
     def kernel_name(self):
         return self.lib.rt_kernel_name(self.ctx).decode()
 
+    def tree_info(self):
+        """The walk the next render uses: {"bvh", "nodes", "leaves", "depth", "always", "trained"}."""
+        info = (C.c_uint32 * 6)()
+        check("rt_context_tree_info", self.lib.rt_context_tree_info(self.ctx, info))
+        return dict(zip(("bvh", "nodes", "leaves", "depth", "always", "trained"), [int(x) for x in info]))
+
     def workspace_bytes(self):
         """Device bytes the context's render workspace holds (rt.h "Workspace")."""
         b = C.c_uint64()

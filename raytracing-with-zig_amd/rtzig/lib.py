@@ -23,6 +23,7 @@ EXPORTED = [
     "rt_context_flush",
     "rt_context_fold_pending",
     "rt_kernel_name",
+    "rt_context_tree_info",
     "rt_context_workspace_bytes",
     "rt_context_enable_timing",
     "rt_context_kernel_times",
@@ -73,6 +74,7 @@ def _declare(lib):
         "rt_context_flush": (C.c_int, [vp]),
         "rt_context_fold_pending": (C.c_int, [vp, P(C.c_int)]),
         "rt_kernel_name": (C.c_char_p, [vp]),
+        "rt_context_tree_info": (C.c_int, [vp, P(C.c_uint32)]),
         "rt_context_workspace_bytes": (C.c_int, [vp, P(C.c_uint64)]),
         "rt_context_enable_timing": (C.c_int, [vp, C.c_int]),
         "rt_context_kernel_times": (C.c_int, [vp, P(C.c_double), P(C.c_double)]),

@@ -2,7 +2,9 @@
 
 * bit-exact against oracle B (the reference arithmetic with the GPU's per-(pixel, sample) streams),
   in both unit modes (ring: in-kernel ordered accumulation; direct: stored samples + reduce pass):
-  config 2 whole image at 100 spp; configs 3 and 4 on 8 interleaved rows at 500 spp; config 5 on one
+  config 2 whole image at 100 spp; configs 3 and 4 on 8 interleaved rows at 500 spp (config 4 on
+  the SAH tree and on the bench's trained tree); config 4's whole frame as bench.py runs it (one
+  launch, trained tree, ring mode) at 100 and at its stated 500 spp; config 5 on one
   row at 10000 spp (2439 sample chunks: the in-kernel ordered accumulation hands each pixel's running
   sum from unit to unit, camera.zig:133-136);
 * statistical against the reference's OWN images (SURVEY §8(c) ladder 3) for configs 2 and 3, whose
@@ -25,7 +27,9 @@ def _box_rmse(a, b):
     return float(np.sqrt(((box(a) - box(b)) ** 2).mean()))
 
 
-def _rows(cam, row0, step, n):
+def _rows(cam, row0, step, n, info=None):
+    """Renders rows row0 + k*step, k < n, in one launch; `info` (a dict) receives the kernel name and
+    the walk the launch used (rt_context_tree_info)."""
     import torch
     r = rtzig.DeviceRenderer(0)
     r.set_scene(cam.scene.world)
@@ -35,6 +39,8 @@ def _rows(cam, row0, step, n):
     r.render_rows_async(cam.cam, buf.data_ptr(), row0=row0, row_step=step, n_rows=n, d_stats_ptr=stats.data_ptr())
     r.sync()
     launches = r.kernel_times_total()[2]
+    if info is not None:
+        info.update(r.tree_info(), kernel=r.kernel_name(), workspace=r.workspace_bytes())
     r.close()
     return buf.cpu().numpy(), [int(x) for x in stats.cpu().tolist()], launches
 
@@ -78,16 +84,44 @@ def test_config3_rows_500spp_bit_exact(oracle, mode, monkeypatch):
     assert st == [rays, 8 * 1200 * 500]
 
 
+@pytest.mark.parametrize("train", ["sah", "trained"])
 @pytest.mark.parametrize("mode", ["ring", "direct"])
-def test_config4_rows_500spp_bit_exact(oracle, mode, monkeypatch):
-    """Config 4 (the bench workload): final scene, 1200x800, 500 spp — 8 rows spread over the image."""
+def test_config4_rows_500spp_bit_exact(oracle, mode, train, monkeypatch):
+    """Config 4 (the bench workload): final scene, 1200x800, 500 spp — 8 rows spread over the image,
+    on the SAH tree an 8-row launch builds by itself (4.8e6 samples, below the 2^25 training
+    threshold) and on the tree trained on the 1200x800 camera's rays — the bench frame's tree
+    (RTZIG_BVH_TRAIN=1; the training depends on the camera, not on the rows or the spp)."""
     monkeypatch.setenv("RTZIG_UNIT_MODE", mode)
+    monkeypatch.setenv("RTZIG_BVH_TRAIN", "1" if train == "trained" else "0")
     cam = rtzig.final_scene_camera(width=1200, aspect_ratio=1.5, spp=500)
     assert (cam.width, cam.height, len(cam.scene.world)) == (1200, 800, 485)
-    out, st, _ = _rows(cam, 7, 99, 8)
+    info = {}
+    out, st, _ = _rows(cam, 7, 99, 8, info)
+    assert info["bvh"] == 1 and info["trained"] == (train == "trained"), info
     ref, rays = oracle.render_b(cam.cam, cam.scene.world, row0=7, row_step=99, n_rows=8, threads=16)
     assert np.array_equal(out, ref)
     assert st == [rays, 8 * 1200 * 500]
+
+
+@pytest.mark.parametrize("spp", [100, 500])
+def test_config4_full_frame_bench_state_bit_exact(oracle, spp):
+    """The bench's exact kernel state against the oracle, every pixel (reference: the row loop of
+    camera.zig:123-145, HittableList.hit's first-wins scan hittable.zig:64-77): the whole 1200x800
+    frame in ONE launch with the library's own choices — 9.6e7 / 4.8e8 samples, so the tree is the
+    one trained on this camera's rays and the launch runs ring mode (its samples exceed direct
+    mode's 2 GiB): the in-kernel ordered accumulation over 15 000 tiles, the LDS tree kernel
+    `bvh_lds`, the chunk schedule of the stated spp.  500 spp is BASELINE config 4 itself, the
+    frame bench.py times; oracle B on 16 host threads takes ~10 / ~45 s."""
+    assert "RTZIG_UNIT_MODE" not in os.environ and "RTZIG_BVH_TRAIN" not in os.environ
+    cam = rtzig.final_scene_camera(width=1200, aspect_ratio=1.5, spp=spp)
+    info = {}
+    out, st, launches = _rows(cam, 0, 1, 800, info)
+    assert launches == 1
+    assert info["kernel"] == "bvh_lds" and info["bvh"] == 1 and info["trained"] == 1, info
+    assert info["workspace"] < 1 << 30, info  # ring + sums (~0.6 GiB), not direct mode's per-sample store
+    ref, rays = oracle.render_b(cam.cam, cam.scene.world, threads=16)
+    assert np.array_equal(out, ref), int((out != ref).any(axis=2).sum())
+    assert st == [rays, 1200 * 800 * spp]
 
 
 @pytest.mark.parametrize("mode", ["ring", "direct"])
