@@ -31,7 +31,7 @@ extern "C" {
 
 #define RT_ABI_VERSION 3
 /* uint64 words of the d_stats buffer of an instrumented render (rt_context_enable_profile) */
-#define RT_PROFILE_STATS_WORDS 32
+#define RT_PROFILE_STATS_WORDS 64
 
 /* ---- status codes ---------------------------------------------------------------------------- */
 typedef enum rt_status {
@@ -214,7 +214,7 @@ int rt_context_kernel_times(rt_context* ctx, double* sample_ms, double* reduce_m
  * *n_launches = the number of sample-kernel launches summed. */
 int rt_context_kernel_times_total(rt_context* ctx, double* sample_ms, double* reduce_ms, uint32_t* n_launches);
 /* Instrumented kernels (diagnostics): when enabled, `d_stats` of rt_render_rows_async must hold
- * RT_PROFILE_STATS_WORDS (32) uint64: {rays, samples, sphere tests executed, BVH node visits, wave-cycles in queue refill,
+ * RT_PROFILE_STATS_WORDS (64) uint64: {rays, samples, sphere tests executed, BVH node visits, wave-cycles in queue refill,
  * wave-cycles in the closest-hit walk, wave-cycles in shading, wave-iterations of the BVH inner
  * (internal-node) loop, wave-iterations of BVH leaf rounds, wave-level candidate blocks (sqrt +
  * root division), wave-level second-root divisions, node visits of camera rays, sphere tests of
@@ -224,8 +224,16 @@ int rt_context_kernel_times_total(rt_context* ctx, double* sample_ms, double* re
  * waves of (wave end - the wave's first empty claim), [22] the last wave's first empty claim, [23..25]
  * the parts of [4]: wave-cycles finalising units, handing out items (claims), seeding + getRay;
  * [26..31] wave-level executions: loop iterations, rejection trips, seeding blocks, walks started
- * (always-list tests), shading blocks, unit finalisations}.  Counts 0-3 are exact and deterministic;
- * the cycles and wave-level counts are diagnostics. */
+ * (always-list tests), shading blocks, unit finalisations; then lane-level executions (the active
+ * lanes summed over every wave-level execution of a block) and the wave-level executions they pair
+ * with: [32] seeding lanes, [33] rejection-trip lanes, [34] / [35] scatter-finish waves / lanes,
+ * [36] / [37] defocus camera-finish waves / lanes, [38] / [39] walk waves / lanes (resumed walks
+ * included), [40] walk-start lanes, [41] shading lanes, [42..47] waves / lanes of the sky, Lambertian
+ * + metal and dielectric shading branches, [48] / [49] store waves / lanes, [50] lanes holding a path
+ * after the hand-out (per iteration), [51] leaf-round lanes, [52] candidate-block lanes, [53]
+ * second-root lanes, [54..57] / [58..61] always-list candidate blocks per always-list slot 0..3, waves
+ * / lanes, [62] / [63] always-list second-root waves / lanes}.  Counts 0-3 are exact and
+ * deterministic; the cycles, wave-level and lane-level counts are diagnostics. */
 int rt_context_enable_profile(rt_context* ctx, int enable);
 
 /* ---- host mirror of the reference's Scene / CameraBuilder / Color / PPM ---------------------- */

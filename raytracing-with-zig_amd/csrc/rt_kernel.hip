@@ -280,32 +280,95 @@ __device__ __forceinline__ uint32_t rank_in(uint64_t mask) {
 // sphere tests, BVH node visits and per-wave shader-clock cycles spent in refill / walk / shade.
 // The counts are deterministic functions of the inputs; the cycles are diagnostics only.
 // ------------------------------------------------------------------------------------------------
-template <bool kOn>
+// kLevel 1: exact counts (sphere tests, node visits) and wave-level executions; kLevel 2 (the
+// instrumented ring-mode kernel, round 6) adds lane-level counts: every lane that executes a block
+// counts itself, so a block's lane count / its wave count is the mean number of active lanes (exec)
+// its instructions run with.  Per-lane counters are 32-bit (a launch's per-lane counts stay far below
+// 2^32).  The instrumented direct-mode kernel keeps level 1: the lane counters would cost it scratch.
+template <int kLevel>
 struct Prof {
     __device__ __forceinline__ void tests(uint32_t) {}
     __device__ __forceinline__ void visit() {}
     __device__ __forceinline__ void inner_iter() {}
     __device__ __forceinline__ void leaf_iter() {}
+    template <int Q>
     __device__ __forceinline__ void cand_block() {}
+    template <int Q>
     __device__ __forceinline__ void root2_block() {}
 };
 template <>
-struct Prof<true> {
-    uint64_t n_tests = 0, n_visits = 0;
-    uint64_t cam_visits = 0, cam_tests = 0;  // of camera rays (bounce 0)
-    uint64_t w_inner = 0, w_leaf = 0;  // wave-level iterations (counted by the first active lane)
-    uint64_t w_cand = 0, w_root2 = 0;  // wave-level candidate blocks (sqrt + root1 division) / root2 divisions
+struct Prof<1> {
+    uint32_t n_tests = 0, n_visits = 0;      // n_visits: lane-level inner steps
+    uint32_t cam_visits = 0, cam_tests = 0;  // of camera rays (bounce 0)
+    uint32_t w_inner = 0, w_leaf = 0;  // wave-level iterations (counted by the first active lane)
+    uint32_t w_cand = 0, w_root2 = 0;  // wave-level candidate blocks (sqrt + root1 division) / root2 divisions
     __device__ __forceinline__ void tests(uint32_t n) { n_tests += n; }
     __device__ __forceinline__ void visit() { ++n_visits; }
-    __device__ __forceinline__ static bool leader() {
+    __device__ __forceinline__ static uint32_t leader() {
         const uint64_t m = __ballot(1);
-        return (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u)) == 0;
+        return (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u)) == 0 ? 1u : 0u;
     }
-    __device__ __forceinline__ void inner_iter() { w_inner += leader() ? 1 : 0; }
-    __device__ __forceinline__ void leaf_iter() { w_leaf += leader() ? 1 : 0; }
-    __device__ __forceinline__ void cand_block() { w_cand += leader() ? 1 : 0; }
-    __device__ __forceinline__ void root2_block() { w_root2 += leader() ? 1 : 0; }
+    __device__ __forceinline__ void inner_iter() { w_inner += leader(); }
+    __device__ __forceinline__ void leaf_iter() { w_leaf += leader(); }
+    template <int Q>
+    __device__ __forceinline__ void cand_block() { w_cand += leader(); }
+    template <int Q>
+    __device__ __forceinline__ void root2_block() { w_root2 += leader(); }
 };
+template <>
+struct Prof<2> : Prof<1> {
+    uint32_t l_leaf = 0, l_cand = 0, l_root2 = 0;  // lane-level leaf rounds, candidate blocks, root2 divisions
+    // the always-list's share: candidate blocks per always-list sphere q < 4 (wave / lane level), and
+    // their second-root divisions
+    uint32_t w_acand[4] = {0, 0, 0, 0}, l_acand[4] = {0, 0, 0, 0}, w_aroot2 = 0, l_aroot2 = 0;
+    __device__ __forceinline__ void leaf_iter() {
+        w_leaf += leader();
+        ++l_leaf;
+    }
+    template <int Q>
+    __device__ __forceinline__ void cand_block() {
+        const uint32_t ld = leader();
+        w_cand += ld;
+        ++l_cand;
+        if constexpr (Q >= 0 && Q < 4) {
+            w_acand[Q] += ld;
+            ++l_acand[Q];
+        }
+    }
+    template <int Q>
+    __device__ __forceinline__ void root2_block() {
+        const uint32_t ld = leader();
+        w_root2 += ld;
+        ++l_root2;
+        if constexpr (Q >= -1) {
+            w_aroot2 += ld;
+            ++l_aroot2;
+        }
+    }
+};
+
+// Region markers of the candidate block (RTZIG_MARKS builds, tools/region_table.py): Q = 0..3 the
+// unrolled always-list spheres, -1 the always-list loop (more than 4), -2 a leaf round.
+template <int Q>
+__device__ __forceinline__ void mark_cand() {
+    if constexpr (Q == 0) RTK_MARK("acand0");
+    else if constexpr (Q == 1) RTK_MARK("acand1");
+    else if constexpr (Q == 2) RTK_MARK("acand2");
+    else if constexpr (Q == 3) RTK_MARK("acand3");
+    else if constexpr (Q == -1) RTK_MARK("acandN");
+    else RTK_MARK("lcand");
+}
+template <int Q>
+__device__ __forceinline__ void mark_root2() {
+    if constexpr (Q >= 0) RTK_MARK("aroot2");
+    else if constexpr (Q == -1) RTK_MARK("aroot2N");
+    else RTK_MARK("lroot2");
+}
+template <int Q>
+__device__ __forceinline__ void mark_caller() {
+    if constexpr (Q >= -1) RTK_MARK("always");
+    else RTK_MARK("leaf");
+}
 
 // ------------------------------------------------------------------------------------------------
 // Closest-hit walkers.  Both return the ORIGINAL list index of the winning sphere (or -1) and its
@@ -542,7 +605,7 @@ struct BvhWalker {
                                                 double& closest, uint32_t& best, bool& found, PR& pr) const {
         u32x8 w;
         asm volatile("s_load_dwordx8 %0, %1, 0\n\ts_waitcnt lgkmcnt(0)" : "=s"(w) : "s"(ageo + q));
-        test_always_geo(w, asid[q], r, a, ad, t_min, lfilt, closest, best, found, pr);
+        test_always_geo<-1>(w, asid[q], r, a, ad, t_min, lfilt, closest, best, found, pr);
     }
     // the same for a compile-time Q < 4 (the unrolled common case): the always-list pointers are
     // re-read from the kernarg segment (BvhArgs, the kernel's second argument) and the sphere sits
@@ -563,7 +626,7 @@ struct BvhWalker {
         uint32_t sid;
         asm volatile("s_load_dwordx8 %0, %2, %3\n\ts_load_dword %1, %4, %5\n\ts_waitcnt lgkmcnt(0)"
                      : "=s"(w), "=s"(sid) : "s"(pg), "i"(Q * 32), "s"(ps), "i"(Q * 4));
-        test_always_geo(w, sid, r, a, ad, t_min, lfilt, closest, best, found, pr);
+        test_always_geo<Q>(w, sid, r, a, ad, t_min, lfilt, closest, best, found, pr);
     }
     __device__ __forceinline__ static uint32_t n_always_now() {
         static_assert(offsetof(BvhArgs, n_always) == 40, "kernarg offset of BvhArgs::n_always");
@@ -572,7 +635,7 @@ struct BvhWalker {
         asm volatile("s_load_dword %0, %1, %2\n\ts_waitcnt lgkmcnt(0)" : "=s"(n) : "s"(kp), "i"(336 + 40));
         return n;
     }
-    template <class PR>
+    template <int Q, class PR>  // Q: the always-list slot when compile-time (instrumented counts), else -1
     __device__ __forceinline__ static void test_always_geo(const u32x8& w, uint32_t sid, const Ray& r, double a, const RayDiv& ad,
                                                            double t_min, const LeafFilter& lfilt, double& closest,
                                                            uint32_t& best, bool& found, PR& pr) {
@@ -584,30 +647,36 @@ struct BvhWalker {
         const double c = ((ocx * ocx + ocy * ocy) + ocz * ocz) - s.r2;
         const double disc = h * h - a * c;
         // the ground sphere is "behind" every ray that leaves it: no sqrt / second-root division
-        if (disc >= 0 && !lfilt.behind(h, disc)) candidate(sid, h, disc, ad, t_min, closest, best, found, pr);
+        if (disc >= 0 && !lfilt.behind(h, disc)) candidate<Q>(sid, h, disc, ad, t_min, closest, best, found, pr);
     }
 
     // root selection of sphere.zig:35-41 for a sphere with disc >= 0, then the first-wins argmin.
     // The argmin is order-independent (ties go to the lower original index), so candidates may be
     // taken in any order.  (A branch-free form that computes both roots for every lane measured 4%
     // slower.)
-    template <class PR>
+    // Q: the always-list slot 0..3, -1 (always-list loop) or -2 (a leaf round): instrumented counts
+    // and region markers only
+    template <int Q, class PR>
     __device__ __forceinline__ static void candidate(uint32_t k, double h, double disc, const RayDiv& a, double t_min,
                                                      double& closest, uint32_t& best, bool& found, PR& pr) {
-        pr.cand_block();
+        mark_cand<Q>();
+        pr.template cand_block<Q>();
         const double sq = sqrt_g(disc);
         double ts = a.div(h - sq);
         bool cand = t_min < ts;
         if (!cand) {
-            pr.root2_block();
+            mark_root2<Q>();
+            pr.template root2_block<Q>();
             ts = a.div(h + sq);
             cand = t_min < ts;
+            mark_cand<Q>();
         }
         if (cand && (ts < closest || (found && ts == closest && k < best))) {
             closest = ts;
             best = k;
             found = true;
         }
+        mark_caller<Q>();
     }
 
     static constexpr bool kCanSuspend = true;
@@ -887,6 +956,7 @@ struct BvhWalker {
         }
         const LeafFilter lfilt = LeafFilter::make(a, t_min);
         const RayDiv ad(a);
+        RTK_MARK("always");
         if (kSusp && resume) {
             // the always-list and the far-origin check ran when this walk started
         } else if (n_always <= 4) {
@@ -902,6 +972,7 @@ struct BvhWalker {
             for (uint32_t q = 0; q < n_always; ++q) test_always(q, r, a, ad, t_min, lfilt, closest, best, found, pr);
         }
         if (!(kSusp && resume)) pr.tests(n_always);
+        RTK_MARK("walk_setup");
 
         // f32 ray for the conservative slab tests (error budget: rt_bvh.cpp)
         const float ox = (float)r.orig.x, oy = (float)r.orig.y, oz = (float)r.orig.z;
@@ -1000,10 +1071,10 @@ struct BvhWalker {
                     const bool p1 = v1 && (!v0 || h[1] < h[0]);  // round 1 takes slot 1
                     const uint32_t s0 = lf->sid[0], s1 = lf->sid[1];
                     if (v0 || v1)
-                        candidate(p1 ? s1 : s0, p1 ? h[1] : h[0], p1 ? disc[1] : disc[0], ad, t_min, closest, best,
+                        candidate<-2>(p1 ? s1 : s0, p1 ? h[1] : h[0], p1 ? disc[1] : disc[0], ad, t_min, closest, best,
                                   found, pr);
                     if (v0 && v1)  // round 2: the other slot
-                        candidate(p1 ? s0 : s1, p1 ? h[0] : h[1], p1 ? disc[0] : disc[1], ad, t_min, closest, best,
+                        candidate<-2>(p1 ? s0 : s1, p1 ? h[0] : h[1], p1 ? disc[0] : disc[1], ad, t_min, closest, best,
                                   found, pr);
                 } else {
                 bool v[kLeafBvh];
@@ -1029,7 +1100,7 @@ struct BvhWalker {
                         any = any || v[u];
                     }
                     if (!any) break;
-                    candidate(kb, hb, db, ad, t_min, closest, best, found, pr);
+                    candidate<-2>(kb, hb, db, ad, t_min, closest, best, found, pr);
                     if (rd + 1 < kLeafBvh) {
 #pragma unroll
                         for (int u = 0; u < kLeafBvh; ++u) {
@@ -1236,13 +1307,20 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
     typename Walker::State ws;  // a suspended walk (dynamic fetch, kSusp only)
     bool susp = false;          // this lane's walk is suspended
     uint64_t rays = 0, nsamples = 0;
-    Prof<kProf> pr;
+    constexpr bool kLanes = kProf && !kDirect;  // lane-level counts (ring mode only, see Prof)
+    Prof<kLanes ? 2 : (kProf ? 1 : 0)> pr;
     uint64_t cyc_refill = 0, cyc_walk = 0, cyc_shade = 0, cyc_trips = 0;  // wave-uniform (kProf only)
     uint64_t cyc_fin = 0, cyc_hand = 0, cyc_seed = 0;  // parts of cyc_refill: finalise, hand-out, seed + getRay
     // wave-level executions (kProf only; scalar, wave-uniform): loop iterations, trip-loop trips, seeding
     // blocks, walks started (always-list tests), shading blocks, finalisations — with the per-step counts
     // of Prof they weight the static instruction counts of each region (tools/region_table.py)
     uint32_t n_iter = 0, n_trip = 0, n_seed = 0, n_wstart = 0, n_shade = 0, n_fin = 0;
+    // lane-level executions (kProf only; wave-uniform sums of ballot popcounts): with the wave-level
+    // counts they give each block's mean active lanes (stats[32..63], tools/region_table.py)
+    uint32_t l_seed = 0, l_trip = 0, w_scat = 0, l_scat = 0, w_camf = 0, l_camf = 0, w_walk = 0, l_walk = 0,
+             l_wstart = 0, l_shade = 0, w_sky = 0, l_sky = 0, w_lm = 0, l_lm = 0, w_di = 0, l_di = 0, w_store = 0,
+             l_store = 0, l_busy = 0;
+    uint32_t sh_kind = 3;  // kProf: this iteration's shading branch (0 sky, 1 Lambertian / metal, 2 dielectric, 3 none)
     uint64_t rt_start = 0, rt_drain = 0;  // s_memrealtime (100 MHz) at start / first empty claim (kProf only)
     if constexpr (kProf) rt_start = __builtin_amdgcn_s_memrealtime();
 
@@ -1289,6 +1367,10 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
         // the lanes handed an item above start their path: seeding and getRay run once, outside
         // the claim loop, so the generator state and ray are not loop-carried through it
         if constexpr (kProf) n_seed += __ballot(fresh) != 0 ? 1u : 0u;
+        if constexpr (kLanes) {
+            l_seed += (uint32_t)__popcll(__ballot(fresh));
+            l_busy += (uint32_t)__popcll(__ballot(active));
+        }
         RTK_MARK("seed");
         if (fresh) {
             const uint32_t row_local = fastdiv(fq, p.div_width);
@@ -1336,8 +1418,10 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
         // scratch memory.)
 #define RTK_TRIP_BODY                                                                   \
     const bool wr = pending && !got, wd = dpend && !dgot;                               \
-    if (__ballot(wr || wd) == 0) break;                                                 \
+    const uint64_t trip_m = __ballot(wr || wd);                                         \
+    if (trip_m == 0) break;                                                             \
     if constexpr (kProf) ++n_trip;                                                      \
+    if constexpr (kLanes) l_trip += (uint32_t)__popcll(trip_m);                         \
     if constexpr (kF32) {                                                               \
         if (wr || wd) trip_f32(g, wr, ux, uy, uz, uls, got, dgot);                      \
     } else if (wr || wd) {                                                              \
@@ -1367,13 +1451,23 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
         }
 #undef RTK_TRIP_BODY
         RTK_MARK("scatter_finish");
+        if constexpr (kLanes) {
+            const uint64_t mg = __ballot(got), md = __ballot(dgot);
+            w_scat += mg != 0 ? 1u : 0u;
+            l_scat += (uint32_t)__popcll(mg);
+            w_camf += md != 0 ? 1u : 0u;
+            l_camf += (uint32_t)__popcll(md);
+        }
         if (dgot) {
+            RTK_MARK("cam_finish");
             camera_finish(ux, uy, r);
             dpend = false;
+            RTK_MARK("scatter_finish");
         }
         if constexpr (kF32) {
             if (got) scatter_f32(ux, uy, uz, uls, sc_metal, sc_nrm, sc_refl, sc_fuzz, pending, done, r, bounce);
         } else if (got) {  // finish the scatter
+            RTK_MARK("scat_finish");
             const double l = sqrt_normal(uls);  // |p|^2 in (1e-160, 1] (vec.zig:76)
             const SharedRcp rl(l);
             const v3 ruv = mk(rl.div(ux), rl.div(uy), rl.div(uz));  // p / sqrt(|p|^2), true divisions
@@ -1404,7 +1498,15 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
         bool shaded = false;  // kProf: this lane ran the shading below
         if constexpr (kProf) {
             const bool walks = active && !done && !pending && !dpend && bounce < p.bounce_max;
-            n_wstart += __ballot(walks && !susp) != 0 ? 1u : 0u;
+            const uint64_t ms = __ballot(walks && !susp);
+            n_wstart += ms != 0 ? 1u : 0u;
+            if constexpr (kLanes) {
+                const uint64_t mw = __ballot(walks);
+                l_wstart += (uint32_t)__popcll(ms);
+                w_walk += mw != 0 ? 1u : 0u;
+                l_walk += (uint32_t)__popcll(mw);
+                sh_kind = 3;
+            }
         }
         if (active && !done && !pending && !dpend) {
             if (bounce >= p.bounce_max) {
@@ -1467,6 +1569,7 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
                 // a metal lane's ray.dir is not read again before its scatter finishes (it then
                 // takes sc_refl + fuzz * ruv), so the reflected direction replaces it in place
                 if (hit && kind == 1) r.dir = reflect(r.dir, nrm);
+                if constexpr (kLanes) sh_kind = hit ? (kind <= 1 ? 1u : 2u) : 0u;
                 const v3 u = unit(r.dir);
                 // The scatter state is read only while `pending`, and a shaded lane was not
                 // pending: every shaded lane takes it (and the hit point as its next origin; a sky
@@ -1478,6 +1581,7 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
                 r.orig = pt;
                 if (!hit) {
                     // sky gradient (camera.zig:171-177)
+                    RTK_MARK("sky");
                     const double a = 0.5 * (u.y + 1.0);
                     const v3 sky = muls(mk(1, 1, 1), 1.0 - a) + muls(mk(0.5, 0.7, 1), a);
                     col = att * sky;
@@ -1486,9 +1590,11 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
                     // Lambertian (material.zig:27-39) / Metal (:55-68): attenuation = albedo.  A
                     // metal ray that ends up absorbed returns black whatever `att` is, so the
                     // product can be taken now.
+                    RTK_MARK("lam_metal");
                     att = att * mk(m.albedo[0], m.albedo[1], m.albedo[2]);
                     pending = true;
                 } else {  // Dielectric.scatter (material.zig:82-110), attenuation (1,1,1)
+                    RTK_MARK("dielectric");
                     const v3 ud = u;
                     const double cos_t = __builtin_fmin(dot(-ud, nrm), 1.0);
                     const double sin_t = sqrt_g(1.0 - cos_t * cos_t);
@@ -1499,11 +1605,25 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
                     r.dir = dir;
                     ++bounce;
                 }
+                RTK_MARK("shade");
                 }
             }
         }
         __builtin_amdgcn_s_setprio(0);
         if constexpr (kProf) n_shade += __ballot(shaded) != 0 ? 1u : 0u;
+        if constexpr (kLanes) {
+            l_shade += (uint32_t)__popcll(__ballot(shaded));
+            const uint64_t m0 = __ballot(shaded && sh_kind == 0), m1 = __ballot(shaded && sh_kind == 1),
+                           m2 = __ballot(shaded && sh_kind == 2), md = __ballot(done);
+            w_sky += m0 != 0 ? 1u : 0u;
+            l_sky += (uint32_t)__popcll(m0);
+            w_lm += m1 != 0 ? 1u : 0u;
+            l_lm += (uint32_t)__popcll(m1);
+            w_di += m2 != 0 ? 1u : 0u;
+            l_di += (uint32_t)__popcll(m2);
+            w_store += md != 0 ? 1u : 0u;
+            l_store += (uint32_t)__popcll(md);
+        }
         RTK_MARK("store");
         if (done) {
             us.store(myslot, mi, col.x, col.y, col.z);
@@ -1600,6 +1720,24 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
                 atomicAdd(&stats[29], (unsigned long long)n_wstart);
                 atomicAdd(&stats[30], (unsigned long long)n_shade);
                 atomicAdd(&stats[31], (unsigned long long)n_fin);
+            }
+        }
+        if constexpr (kLanes) {
+            if (lane == 0) {
+                const uint32_t wu[19] = {l_seed, l_trip, w_scat, l_scat, w_camf, l_camf, w_walk, l_walk, l_wstart,
+                                         l_shade, w_sky, l_sky, w_lm, l_lm, w_di, l_di, w_store, l_store, l_busy};
+#pragma unroll
+                for (int k = 0; k < 19; ++k) atomicAdd(&stats[32 + k], (unsigned long long)wu[k]);
+            }
+            // the walker's per-lane counts (leaf rounds, candidate blocks, always-list parts), summed
+            // over the wave: stats[51..63]
+            uint32_t pl[13] = {pr.l_leaf, pr.l_cand, pr.l_root2, pr.w_acand[0], pr.w_acand[1], pr.w_acand[2],
+                               pr.w_acand[3], pr.l_acand[0], pr.l_acand[1], pr.l_acand[2], pr.l_acand[3], pr.w_aroot2,
+                               pr.l_aroot2};
+#pragma unroll
+            for (int k = 0; k < 13; ++k) {
+                for (int off = 32; off > 0; off >>= 1) pl[k] += __shfl_xor(pl[k], off, 64);
+                if (lane == 0) atomicAdd(&stats[51 + k], (unsigned long long)pl[k]);
             }
         }
     }

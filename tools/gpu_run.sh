@@ -11,8 +11,8 @@
 #   smoke      __graft_entry__.smoke()
 #   tests      pytest -m gpu, one process, per-test limits                       [PYTEST_ARGS]
 #   bench      the default bench line                                            [BENCH_ARGS]
-#   kprof      instrumented counts of one 100-spp config-4 frame (tools/kprofile.py)  [KPROF_ARGS]
-#   regions    lane-level region counts of the instrumented frame, then the region table
+#   kprof      instrumented counts of one 100-spp config-4 frame, wave- and lane-level per region
+#              (tools/kprofile.py; then here: python tools/region_table.py <kprof.json>)  [KPROF_ARGS]
 #   profile    rocprofv3 kernel trace + separate PMC passes (tools/profile.sh)
 #   ab         tools/ab_libs.py on config 4's whole frame (ring mode) and rank 0 of 8 (direct)  [AB SPP ROUNDS]
 #   ab_ch9     the same on chapter 9 (config 2)                                  [AB ROUNDS]
@@ -43,7 +43,6 @@ for step in "$@"; do
     tests)   run gputest 900 python3 -u -m pytest tests -m gpu -x -v --timeout 150 --timeout-method thread $PYTEST_ARGS ;;
     bench)   run bench 300 python3 -u bench.py $BENCH_ARGS ;;
     kprof)   run kprof 200 python3 -u tools/kprofile.py --spp 100 --variants bvh --out "gpurun_out/kprof_$T.json" $KPROF_ARGS ;;
-    regions) run regions 300 python3 -u tools/kprofile.py --spp 100 --variants bvh --lanes --out "gpurun_out/lanes_$T.json" ;;
     profile) TAG=$T bash tools/profile.sh || exit $? ;;
     ab)      run ab_full 300 python3 -u tools/ab_libs.py $AB --spp ${SPP:-100} --rounds ${ROUNDS:-7}
              run ab_r8 300 python3 -u tools/ab_libs.py $AB --spp 500 --row-step 8 --rounds ${ROUNDS:-7} ;;

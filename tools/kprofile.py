@@ -15,6 +15,40 @@ import torch  # noqa: E402
 
 import rtzig  # noqa: E402
 
+def lanes_of(s):
+    """Mean active lanes per block (round 6, rt.h stats[32..63] beside the wave-level counts): for each
+    block, its wave-level executions, lane-level executions and their ratio.  None for a kernel
+    without lane counts (direct mode)."""
+    if len(s) < 64 or not s[32]:
+        return None
+    acw, acl = s[54:58], s[58:62]
+
+    def row(w, l):
+        return {"waves": w, "lanes": l, "mean_lanes": round(l / w, 3) if w else None}
+    return {
+        "seed_and_getRay": row(s[28], s[32]),
+        "rejection_trip": row(s[27], s[33]),
+        "scatter_finish": row(s[34], s[35]),
+        "defocus_camera_finish": row(s[36], s[37]),
+        "walk_any (started + resumed)": row(s[38], s[39]),
+        "walk_start (always-list tests, slab setup)": row(s[29], s[40]),
+        "walk_inner_step": row(s[7], s[3]),
+        "leaf_round": row(s[8], s[51]),
+        "candidate_block_all": row(s[9], s[52]),
+        "candidate_block_always_list": {f"q{q}": row(acw[q], acl[q]) for q in range(4)},
+        "candidate_block_leaf": row(s[9] - sum(acw), s[52] - sum(acl)),
+        "root2_all": row(s[10], s[53]),
+        "root2_always_list": row(s[62], s[63]),
+        "root2_leaf": row(s[10] - s[62], s[53] - s[63]),
+        "shade": row(s[30], s[41]),
+        "shade_sky": row(s[42], s[43]),
+        "shade_lambertian_metal": row(s[44], s[45]),
+        "shade_dielectric": row(s[46], s[47]),
+        "store": row(s[48], s[49]),
+        "lanes_holding_a_path_per_iteration": row(s[26], s[50]),
+    }
+
+
 res_waves = torch.cuda.get_device_properties(0).multi_processor_count * 16 if torch.cuda.is_available() else 4096  # persistent grid: 16 waves per CU
 ap = argparse.ArgumentParser()
 ap.add_argument("--width", type=int, default=1200)
@@ -88,6 +122,7 @@ for v in args.variants.split():
                         "trips_per_iter": round(s[27] / s[26], 3), "seed_blocks_per_iter": round(s[28] / s[26], 3),
                         "walk_starts_per_iter": round(s[29] / s[26], 3), "shade_blocks_per_iter": round(s[30] / s[26], 3),
                         "finalisations": s[31], "samples_per_iter": round(s[1] / s[26], 3)} if s[26] else None),
+        "lanes": lanes_of(s),
         "raw": s,
     }
     r.enable_profile(False)

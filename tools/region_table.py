@@ -184,28 +184,59 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("kprof")
     ap.add_argument("--spp-scale", type=float, default=5.0, help="frame spp / kprof spp (500 / 100)")
-    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r04", "summary.json"))
+    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r05", "summary.json"))
     ap.add_argument("--asm", default=None, help="price this assembly file instead of compiling (RTZIG_MARKS build)")
     ap.add_argument("--out", default=None)
     ap.add_argument("-D", action="append", default=[], help="extra -D for the build (variants)")
     args = ap.parse_args()
     raw = json.load(open(args.kprof))["variants"]["bvh"]["raw"]
     sc = args.spp_scale
+    lanes_ok = len(raw) >= 64 and raw[32] > 0
     n = {"iter": raw[26] * sc, "trips": raw[27] * sc, "seed": raw[28] * sc, "wstart": raw[29] * sc, "shade": raw[30] * sc,
-         "inner": raw[7] * sc, "leaf": raw[8] * sc, "cand": raw[9] * sc, "root2": raw[10] * sc, "fin": raw[31] * sc,
-         # seed-window passes: only the -DRTZIG_SEED_WINDOW=1 build of commit 2b16cfb has these regions
-         # and counts ([32], [33] of its 40-word stats); otherwise estimated as one per 64 samples
-         "win": (raw[32] - raw[33] if len(raw) > 33 and raw[32] else raw[1] / 64) * sc,
-         "win2": (raw[33] if len(raw) > 33 and raw[32] else raw[1] / 64 / 50) * sc}
+         "inner": raw[7] * sc, "leaf": raw[8] * sc, "cand": raw[9] * sc, "root2": raw[10] * sc, "fin": raw[31] * sc}
+    # Weights (wave-level executions) and mean active lanes per region.  Round 6: the instrumented
+    # kernel also counts, per block, the lanes that execute it (stats[32..63], tools/kprofile.py
+    # "lanes"), and the candidate blocks, scatter finish and shading branches carry markers of their
+    # own, so each sub-region is weighted by its own executions (round 5 weighted every block of a
+    # region by the region's executions: an upper bound).
+    W, LN = {}, {}
+    full = 64.0
+    for r in ("finalise", "fin_work", "handout", "idle", "scatter_finish"):
+        LN[r] = full
+    if lanes_ok:
+        g = lambda k: raw[k] * sc  # noqa: E731
+        acw, acl = [g(54 + q) for q in range(4)], [g(58 + q) for q in range(4)]
+        lcw, lcl = g(9) - sum(acw), g(52) - sum(acl)
+        ratio = lambda l, w: l / w if w else 0.0  # noqa: E731
+        W.update({"walk_setup": g(38), "always": n["wstart"], "cam_finish": g(36), "scat_finish": g(34),
+                  "sky": g(42), "lam_metal": g(44), "dielectric": g(46), "store": g(48), "aroot2N": 0.0, "acandN": 0.0})
+        for q in range(4):
+            W[f"acand{q}"] = acw[q]
+            LN[f"acand{q}"] = ratio(acl[q], acw[q])
+        LN.update({"seed": ratio(g(32), g(28)), "trips": ratio(g(33), g(27)), "cam_finish": ratio(g(37), g(36)),
+                   "scat_finish": ratio(g(35), g(34)), "walk_setup": ratio(g(39), g(38)), "always": ratio(g(40), g(29)),
+                   "walk_inner": ratio(g(3), g(7)), "walk_inner_other": ratio(g(39), g(38)), "leaf": ratio(g(51), g(8)),
+                   "lcand": ratio(lcl, lcw), "aroot2": ratio(g(63), g(62)), "lroot2": ratio(g(53) - g(63), g(10) - g(62)),
+                   "shade": ratio(g(41), g(30)), "sky": ratio(g(43), g(42)), "lam_metal": ratio(g(45), g(44)),
+                   "dielectric": ratio(g(47), g(46)), "store": ratio(g(49), g(48))})
+        n.update({"lcand_total": lcw, "aroot2_total": g(62), "lroot2_total": g(10) - g(62), "walk_any": g(38)})
     lines = open(args.asm).read().split("\n") if args.asm else asm(["-DRTZIG_MARKS=1"] + ["-D" + d for d in args.D])
     blocks = blocks_of(lines, KERNEL)
     per, succ = regions(blocks)
+    # copies of an inlined candidate block: marker occurrences (entry + the re-entry after the root2
+    # branch for the candidate markers), so each copy gets its share of the region's executions
+    nmarks = collections.Counter(m for b in blocks for _, m in b["marks"])
+    copies = {"lcand": nmarks["lcand"] / 2, "aroot2": nmarks["aroot2"], "lroot2": nmarks["lroot2"]}
+    if lanes_ok:
+        W["lcand"] = n["lcand_total"] / max(1.0, copies["lcand"])
+        W["aroot2"] = n["aroot2_total"] / max(1.0, copies["aroot2"])
+        W["lroot2"] = n["lroot2_total"] / max(1.0, copies["lroot2"])
     static = collections.defaultdict(lambda: collections.Counter())
     inner_loop = {k for k, ss in succ.items() if k in ss and any(klass(i) == "lds" for i in blocks[k]["ins"])
                   and any(i.startswith("v_pk_fma") for i in blocks[k]["ins"])}
     cand_blocks = {k for k, b in enumerate(blocks) if any(i.startswith("v_rsq_f64") for i in b["ins"])}
     # blocks on a cycle that stays inside walk_setup: the always-list loop for more than 4 spheres
-    ws_blocks = {k for k, r, _ in per if r == "walk_setup"}
+    ws_blocks = {k for k, r, _ in per if r in ("walk_setup", "always")}
     def reach(a):
         seen, todo = set(), [a]
         while todo:
@@ -219,6 +250,7 @@ def main():
     dyn = collections.defaultdict(lambda: collections.Counter())
     table = issue_rates.load(RATES)
     cyc = collections.Counter()    # measured-rate VALU issue cycles per region
+    lcyc = collections.Counter()   # ... x mean active lanes (lane-cycles)
     other = collections.Counter()  # the ops outside the PMC's f64 add/mul/fma and transcendental classes
     opcyc = collections.Counter()  # ... per opcode (whole kernel)
     opcnt = collections.Counter()  # executions per opcode
@@ -230,10 +262,17 @@ def main():
         static[r][c] += 1
         if r in ("rare", "prologue", "epilogue", "?"):
             continue
+        lanes = LN.get(r, full)
         if r == "walk_inner":
-            w = n["inner"] if k in inner_loop else n["leaf"] + n["wstart"]
+            if k in inner_loop:
+                w = n["inner"]
+            else:
+                w = n["leaf"] + (n["walk_any"] if lanes_ok else n["wstart"])
+                lanes = LN.get("walk_inner_other", full)
+        elif r in W:
+            w = 0 if (r in ("walk_setup", "always") and k in ws_loop) else W[r]
         elif r == "leaf":
-            w = n["cand"] - 0.0 if k in cand_blocks else n["leaf"]
+            w = n["cand"] if (k in cand_blocks and not lanes_ok) else n["leaf"]
         elif r == "walk_setup":
             # the always-list loop for more than 4 spheres (self-loop blocks) does not run on a scene
             # with <= 4 always-list spheres (config 4: the ground and three r = 1 spheres)
@@ -243,10 +282,6 @@ def main():
             w = n["trips"] / 3
         elif r == "seed":
             w = n["seed"]
-        elif r == "seed_window":
-            w = n["win"]
-        elif r == "seed_window2":
-            w = n["win2"]
         elif r == "shade":
             w = n["shade"]
         elif r == "fin_work":
@@ -262,18 +297,20 @@ def main():
             if base not in table["opcodes"] and base not in table["fast_rule"]["opcodes"]:
                 unpriced[op] += w
             cyc[r] += w * rt
+            lcyc[r] += w * rt * lanes
+            dyn[r]["valu_lanes"] += w * lanes
             opcyc[op] += w * rt
             opcnt[op] += w
             regop[(r, op)] += w * rt
             why = issue_rates.fast_penalty(ins, table)
             if why and r not in ("rare", "prologue", "epilogue", "?"):
                 pen[(r, op, why)] += w * (rt - table["fast_rule"]["fast"])
-            if r not in ("rare", "prologue", "epilogue", "?") and not re.match(
-                    r"^v_(add|mul|fma|fmac)_f64|^v_(rsq|rcp|sqrt|exp|log|sin|cos)_f(32|64)", op):
+            if not re.match(r"^v_(add|mul|fma|fmac)_f64|^v_(rsq|rcp|sqrt|exp|log|sin|cos)_f(32|64)", op):
                 other["n"] += w
                 other["cyc"] += w * rt
-    order = ["finalise", "fin_work", "handout", "seed", "seed_window", "seed_window2", "idle", "trips", "scatter_finish", "walk_setup", "walk_inner", "leaf", "shade",
-             "store", "rare", "prologue", "epilogue", "?"]
+    order = ["finalise", "fin_work", "handout", "seed", "idle", "trips", "scatter_finish", "cam_finish", "scat_finish",
+             "walk_setup", "always", "acand0", "acand1", "acand2", "acand3", "acandN", "aroot2", "aroot2N", "walk_inner",
+             "leaf", "lcand", "lroot2", "shade", "sky", "lam_metal", "dielectric", "store", "rare", "prologue", "epilogue", "?"]
     rows = []
     tot = collections.Counter()
     for r in order:
@@ -281,19 +318,28 @@ def main():
             continue
         d = dyn.get(r, collections.Counter())
         tot.update(d)
+        valu = d["valu_32"] + d["valu_f64"]
         rows.append({"region": r, "static": dict(static[r]),
-                     "dyn_valu": d["valu_32"] + d["valu_f64"], "dyn_valu_f64": d["valu_f64"], "dyn_salu": d["salu"],
-                     "dyn_lds": d["lds"], "dyn_nop": d["nop"], "valu_issue_cycles_est": cyc.get(r, 0.0)})
+                     "dyn_valu": valu, "dyn_valu_f64": d["valu_f64"], "dyn_salu": d["salu"],
+                     "dyn_lds": d["lds"], "dyn_nop": d["nop"], "valu_issue_cycles_est": cyc.get(r, 0.0),
+                     "mean_active_lanes": round(lcyc[r] / cyc[r], 2) if cyc.get(r) else None})
     tcyc = sum(cyc[r["region"]] for r in rows)
     tval = tot["valu_32"] + tot["valu_f64"]
     for r in rows:
-        r["valu_issue_share"] = round(r["valu_issue_cycles_est"] / tcyc, 4) if tcyc else None
+        c = r["valu_issue_cycles_est"]
+        r["valu_issue_share"] = round(c / tcyc, 4) if tcyc else None
+        if r["mean_active_lanes"] is not None and tcyc:
+            # issue cycles spent on lanes that do nothing: share x (1 - lanes / 64)
+            r["wasted_issue_share"] = round(c / tcyc * (1 - r["mean_active_lanes"] / 64), 4)
     res = {"kernel": "sample_kernel_bvh<true,false,false> (-DRTZIG_MARKS=1 build: " + str(len(per)) + " instructions)",
-           "counts_per_frame": n, "rows": rows,
+           "counts_per_frame": n, "lane_counts": lanes_ok, "region_copies": copies, "rows": rows,
            "total_est": {"valu": tval, "valu_f64": tot["valu_f64"], "salu": tot["salu"],
                          "lds": tot["lds"], "nop": tot["nop"], "valu_issue_cycles": tcyc,
                          "valu_cycles_per_instruction": tcyc / tval if tval else None,
-                         "other_valu_cycles_per_instruction": other["cyc"] / other["n"] if other["n"] else None},
+                         "other_valu_cycles_per_instruction": other["cyc"] / other["n"] if other["n"] else None,
+                         "mean_active_lanes_cycle_weighted": round(sum(lcyc.values()) / tcyc, 2) if tcyc else None,
+                         "mean_active_lanes_instruction_weighted": round(tot["valu_lanes"] / tval, 2) if tval else None,
+                         "wasted_issue_share": round(1 - sum(lcyc.values()) / tcyc / 64, 4) if tcyc else None},
            "rates": {"source": os.path.relpath(RATES, ROOT),
                      "model": "SIMD cycles per wave64 instruction, event-timed per opcode and operand form (round 5)"},
            "top_opcodes_by_issue_cycles": [{"op": o, "cycles": c, "share": round(c / tcyc, 4),
@@ -311,17 +357,19 @@ def main():
                       "valu_f64": pm["SQ_INSTS_VALU_ADD_F64"] + pm["SQ_INSTS_VALU_MUL_F64"] + pm["SQ_INSTS_VALU_FMA_F64"],
                       "source": os.path.relpath(args.pmc, ROOT),
                       "estimate_over_pmc_valu": round(tval / pm["SQ_INSTS_VALU"], 3)}
+        if pm.get("SQ_ACTIVE_INST_VALU"):
+            res["pmc"]["valu_lanes_active_of_64"] = round(pm["SQ_THREAD_CYCLES_VALU"] / pm["SQ_ACTIVE_INST_VALU"], 2)
     except (OSError, KeyError):
         pass
     txt = json.dumps(res, indent=1)
     if args.out:
         open(args.out, "w").write(txt)
-    print(f"{'region':16s} {'static V/S/LDS/nop':>22s} {'dyn VALU':>10s} {'f64':>9s} {'SALU':>9s} {'LDS':>9s} {'issue cyc':>10s} share")
+    print(f"{'region':16s} {'static V/S/LDS/nop':>22s} {'dyn VALU':>10s} {'f64':>9s} {'SALU':>9s} {'LDS':>9s} {'issue cyc':>10s} share lanes wasted")
     for r in rows:
         s = r["static"]
         print(f"{r['region']:16s} {s.get('valu_32', 0) + s.get('valu_f64', 0):5d}/{s.get('salu', 0):4d}/{s.get('lds', 0):3d}/{s.get('nop', 0):3d}"
               f"       {r['dyn_valu']:10.3g} {r['dyn_valu_f64']:9.3g} {r['dyn_salu']:9.3g} {r['dyn_lds']:9.3g} {r['valu_issue_cycles_est']:10.3g}"
-              f" {r['valu_issue_share'] or 0:.3f}")
+              f" {r['valu_issue_share'] or 0:.3f} {r['mean_active_lanes'] or 0:5.1f} {r.get('wasted_issue_share', 0):.3f}")
     print("total est", res["total_est"], "pmc", res.get("pmc"))
 
 
