@@ -31,7 +31,7 @@ extern "C" {
 
 #define RT_ABI_VERSION 3
 /* uint64 words of the d_stats buffer of an instrumented render (rt_context_enable_profile) */
-#define RT_PROFILE_STATS_WORDS 64
+#define RT_PROFILE_STATS_WORDS 72
 
 /* ---- status codes ---------------------------------------------------------------------------- */
 typedef enum rt_status {
@@ -214,7 +214,7 @@ int rt_context_kernel_times(rt_context* ctx, double* sample_ms, double* reduce_m
  * *n_launches = the number of sample-kernel launches summed. */
 int rt_context_kernel_times_total(rt_context* ctx, double* sample_ms, double* reduce_ms, uint32_t* n_launches);
 /* Instrumented kernels (diagnostics): when enabled, `d_stats` of rt_render_rows_async must hold
- * RT_PROFILE_STATS_WORDS (64) uint64: {rays, samples, sphere tests executed, BVH node visits, wave-cycles in queue refill,
+ * RT_PROFILE_STATS_WORDS (72) uint64: {rays, samples, sphere tests executed, BVH node visits, wave-cycles in queue refill,
  * wave-cycles in the closest-hit walk, wave-cycles in shading, wave-iterations of the BVH inner
  * (internal-node) loop, wave-iterations of BVH leaf rounds, wave-level candidate blocks (sqrt +
  * root division), wave-level second-root divisions, node visits of camera rays, sphere tests of
@@ -232,7 +232,8 @@ int rt_context_kernel_times_total(rt_context* ctx, double* sample_ms, double* re
  * + metal and dielectric shading branches, [48] / [49] store waves / lanes, [50] lanes holding a path
  * after the hand-out (per iteration), [51] leaf-round lanes, [52] candidate-block lanes, [53]
  * second-root lanes, [54..57] / [58..61] always-list candidate blocks per always-list slot 0..3, waves
- * / lanes, [62] / [63] always-list second-root waves / lanes}.  Counts 0-3 are exact and
+ * / lanes, [62] / [63] always-list second-root waves / lanes, [64] / [65] seed-window fills / take
+ * passes (RTZIG_SEED_WIN builds), [66..71] unused}.  Counts 0-3 are exact and
  * deterministic; the cycles, wave-level and lane-level counts are diagnostics. */
 int rt_context_enable_profile(rt_context* ctx, int enable);
 

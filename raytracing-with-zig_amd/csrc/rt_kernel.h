@@ -180,7 +180,21 @@ typedef int16_t StackEntry;
 #else
 typedef int32_t StackEntry;
 #endif
-constexpr size_t kLdsSceneBudget = 80 * 1024;  // tree + stacks of one block (2 blocks per CU's 160 KiB)
+// Seed window (RTZIG_SEED_WIN): a wave seeds the generators and pixel sample points
+// of 64 items at once, all lanes busy, into an LDS window its fresh lanes then read — instead of each
+// fresh lane seeding its own (≈21 of 64 lanes active).  Per wave: 14 dword planes of 64 lanes
+// (Xoshiro s0..s3 after sampleSquare's two draws, the pixel sample point): 3.5 KiB.
+#ifndef RTZIG_SEED_WIN
+#define RTZIG_SEED_WIN 0
+#endif
+constexpr bool kSeedWin = RTZIG_SEED_WIN != 0;
+constexpr uint32_t kSeedWinPlanes = 14;
+constexpr uint32_t kSeedWinBytes = kSeedWinPlanes * 64 * 4;
+// LDS of one block: its share of a CU's 160 KiB at 16 waves per CU (2 blocks of 512 threads, or one
+// of 1024), less its waves' seed windows; the rest holds the tree + stacks when they fit
+constexpr size_t kLdsBlockShare = (size_t)160 * 1024 * (size_t)kBlockBvh / 1024;
+constexpr size_t kSeedWinBlockBytes = kSeedWin ? (size_t)(kBlockBvh / 64) * kSeedWinBytes : 0;
+constexpr size_t kLdsSceneBudget = kLdsBlockShare - kSeedWinBlockBytes;  // tree + stacks of one block
 constexpr int kMaxDepthBvh = 16;   // == rtbvh::kMaxDepth: bound on per-lane LDS stack entries (entry 0: "done")
 #ifndef RTZIG_LEAF
 #define RTZIG_LEAF 2

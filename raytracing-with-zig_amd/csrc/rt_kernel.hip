@@ -95,6 +95,46 @@ __device__ __forceinline__ bool camera_start(uint32_t i, uint32_t j, Rng& g, Ray
     r.dir = ps;
     return true;  // the disk sample is pending
 }
+// The seed window's half of camera_start: sampleSquare's draws and the pixel sample point
+// (camera.zig:190-193, 203-209), the same operations as above.
+__device__ __forceinline__ v3 pixel_sample_point(uint32_t i, uint32_t j, Rng& g) {
+    u32x16 A;  // dwords 6..21 of KernelParams: center, pixel0, du.x, du.y
+    u32x8 B;   // dwords 22..29: du.z, dv
+    const uint64_t kp = (uint64_t)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile(
+        "s_load_dwordx16 %0, %2, 24\n\t"
+        "s_load_dwordx8 %1, %2, 88\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=s"(A), "=s"(B)
+        : "s"(kp));
+    const v3 p0 = mk(dw2d(A[6], A[7]), dw2d(A[8], A[9]), dw2d(A[10], A[11]));
+    const v3 du = mk(dw2d(A[12], A[13]), dw2d(A[14], A[15]), dw2d(B[0], B[1]));
+    const v3 dv = mk(dw2d(B[2], B[3]), dw2d(B[4], B[5]), dw2d(B[6], B[7]));
+    const double ox = g.uniform() - 0.5;
+    const double oy = g.uniform() - 0.5;
+    return (p0 + muls(du, (double)i + ox)) + muls(dv, (double)j + oy);
+}
+// ... and the rest, for a fresh lane given its window entry: the ray from the camera center
+// (defocus: the direction holds the sample point until camera_finish adds the disk sample)
+__device__ __forceinline__ bool camera_from_point(const v3& ps, Ray& r) {
+    u32x8 A;  // dwords 6..13: center (+2 unused)
+    u32x2 C;  // dwords 42..43: defocus_angle
+    const uint64_t kp = (uint64_t)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile(
+        "s_load_dwordx8 %0, %2, 24\n\t"
+        "s_load_dwordx2 %1, %2, 168\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=s"(A), "=s"(C)
+        : "s"(kp));
+    const v3 center = mk(dw2d(A[0], A[1]), dw2d(A[2], A[3]), dw2d(A[4], A[5]));
+    r.orig = center;
+    if (dw2d(C[0], C[1]) <= 0) {
+        r.dir = ps - center;
+        return false;
+    }
+    r.dir = ps;
+    return true;
+}
 // rayOrigin = defocusDiskSample() = (center + defocusDiskU * p.x) + defocusDiskV * p.y;
 // rayDirection = pixelSample - rayOrigin
 __device__ __forceinline__ void camera_finish(double px, double py, Ray& r) {
@@ -1277,10 +1317,12 @@ __device__ __forceinline__ void fold_chunks(const FoldArgs& f, uint32_t lane) {
 // samples + the ordered finalisation of finished units.
 // `geo_orig` is the geometry in original list order (hit-record center of the winner).
 // ------------------------------------------------------------------------------------------------
-template <bool kProf, bool kDirect, class Walker>
+// kWin: fresh lanes take their generator and pixel sample point from the wave's seed window in LDS
+// (`win`: its address; kSeedWin builds of the f64 BVH kernel).
+template <bool kProf, bool kDirect, bool kWin = false, class Walker>
 __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& walk, const GeoRec* __restrict__ geo_orig,
                                           const MatRec* __restrict__ mat_g, const UnitArgs& ua,
-                                          unsigned long long* __restrict__ stats) {
+                                          unsigned long long* __restrict__ stats, uint32_t win = 0) {
     const uint32_t W = p.width;
     const uint32_t lane = lane_id();
     UnitSched<kDirect> us(ua, blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64);
@@ -1321,7 +1363,10 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
              l_wstart = 0, l_shade = 0, w_sky = 0, l_sky = 0, w_lm = 0, l_lm = 0, w_di = 0, l_di = 0, w_store = 0,
              l_store = 0, l_busy = 0;
     uint32_t sh_kind = 3;  // kProf: this iteration's shading branch (0 sky, 1 Lambertian / metal, 2 dielectric, 3 none)
+    uint32_t n_fill = 0, n_take = 0;  // kLanes: seed-window fills / take passes (stats[64], [65])
     uint64_t rt_start = 0, rt_drain = 0;  // s_memrealtime (100 MHz) at start / first empty claim (kProf only)
+    // the seed window's key (wave-uniform): the 64 pixels 64 * win_t + l of the launch at sample win_s
+    uint32_t win_t = ~0u, win_s = ~0u;
     if constexpr (kProf) rt_start = __builtin_amdgcn_s_memrealtime();
 
     // Head fold: the previous deferred call's reduce pass (rt_render_rows_async_deferred) is started
@@ -1372,7 +1417,63 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
             l_busy += (uint32_t)__popcll(__ballot(active));
         }
         RTK_MARK("seed");
-        if (fresh) {
+        if constexpr (kWin && !kF32) {
+            // Seed window: the fresh lanes' items are (pixel fq, sample fs); the window holds the
+            // generators (after sampleSquare's draws) and pixel sample points of the 64 pixels
+            // 64 * win_t + l at sample win_s, computed by all 64 lanes at once.  Each pass serves
+            // the fresh lanes of one (pixel group, sample) key, refilling the window first when it
+            // holds another: a hand-out that crosses a sample layer or a unit takes two passes.
+            // Every lane's generator is seeded and drawn exactly as camera_start does, so the bits
+            // are unchanged.
+            typedef __attribute__((address_space(3))) uint32_t lds_u32;
+            lds_u32* wp = (lds_u32*)(uintptr_t)win;
+            uint64_t todo = __ballot(fresh);
+            while (todo != 0) {
+                const uint32_t ld = (uint32_t)__builtin_ctzll(todo);
+                const uint32_t kt = __builtin_amdgcn_readlane(fq >> 6, ld);
+                const uint32_t ks = __builtin_amdgcn_readlane(fs, ld);
+                if (kt != win_t || ks != win_s) {
+                    RTK_MARK("win_fill");
+                    if constexpr (kLanes) ++n_fill;
+                    win_t = kt;
+                    win_s = ks;
+                    const uint32_t q = kt * 64 + lane;  // past the launch's last pixel: computed, never read
+                    const uint32_t row_local = fastdiv(q, p.div_width);
+                    const uint32_t i = q - row_local * W;
+                    const uint32_t j = p.row0 + row_local * p.row_step;
+                    Rng gw;
+                    gw.seed(sample_key(p.seed_mix, (uint64_t)j * W + i, ks));
+                    const v3 ps = pixel_sample_point(i, j, gw);
+                    const uint64_t w[7] = {gw.s0, gw.s1, gw.s2, gw.s3, __builtin_bit_cast(uint64_t, ps.x),
+                                           __builtin_bit_cast(uint64_t, ps.y), __builtin_bit_cast(uint64_t, ps.z)};
+#pragma unroll
+                    for (int k = 0; k < 7; ++k) {
+                        wp[(2 * k) * 64 + lane] = (uint32_t)w[k];
+                        wp[(2 * k + 1) * 64 + lane] = (uint32_t)(w[k] >> 32);
+                    }
+                    RTK_MARK("seed");
+                }
+                if constexpr (kLanes) ++n_take;
+                const bool mine = fresh && (fq >> 6) == kt && fs == ks;
+                if (mine) {
+                    const uint32_t e = fq & 63;
+                    uint64_t w[7];
+#pragma unroll
+                    for (int k = 0; k < 7; ++k)
+                        w[k] = (uint64_t)wp[(2 * k) * 64 + e] | ((uint64_t)wp[(2 * k + 1) * 64 + e] << 32);
+                    g.s0 = w[0];
+                    g.s1 = w[1];
+                    g.s2 = w[2];
+                    g.s3 = w[3];
+                    dpend = camera_from_point(mk(__builtin_bit_cast(double, w[4]), __builtin_bit_cast(double, w[5]),
+                                                 __builtin_bit_cast(double, w[6])),
+                                              r);
+                    att = V{1, 1, 1};
+                    bounce = 0;
+                }
+                todo &= ~__ballot(mine);
+            }
+        } else if (fresh) {
             const uint32_t row_local = fastdiv(fq, p.div_width);
             const uint32_t i = fq - row_local * W;
             const uint32_t j = p.row0 + row_local * p.row_step;
@@ -1728,6 +1829,8 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
                                          l_shade, w_sky, l_sky, w_lm, l_lm, w_di, l_di, w_store, l_store, l_busy};
 #pragma unroll
                 for (int k = 0; k < 19; ++k) atomicAdd(&stats[32 + k], (unsigned long long)wu[k]);
+                atomicAdd(&stats[64], (unsigned long long)n_fill);
+                atomicAdd(&stats[65], (unsigned long long)n_take);
             }
             // the walker's per-lane counts (leaf rounds, candidate blocks, always-list parts), summed
             // over the wave: stats[51..63]
@@ -1800,9 +1903,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kWaves))
         nodes = ln; \
         leaves = ll; \
     } \
-    path_loop<kProf, kDirect>(p, Walker{nodes, leaves, b.always_geo, b.always_sid, b.n_always, stack + threadIdx.x, \
-                                         b.origin_bound, geo_g, p.n_pad RTK_BOUNDS_ARGS}, geo_g, \
-                              mat_g, ua, stats);
+    /* the wave's seed window after the stacks (kSeedWin, f64 kernels) */ \
+    const uint32_t win = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) unsigned char*)( \
+        lds_raw + ((scene_bytes + (size_t)b.stack_depth * kBlockBvh * sizeof(Stack) + 15) & ~(size_t)15) + \
+        (threadIdx.x / 64) * kSeedWinBytes); \
+    path_loop<kProf, kDirect, kSeedWin && !kF32>(p, Walker{nodes, leaves, b.always_geo, b.always_sid, b.n_always, \
+                                         stack + threadIdx.x, b.origin_bound, geo_g, p.n_pad RTK_BOUNDS_ARGS}, geo_g, \
+                              mat_g, ua, stats, win);
 
 template <bool kLdsScene, bool kProf, bool kDirect>
 __global__ __launch_bounds__(kBlockBvh) RTK_BVH_WAVES void sample_kernel_bvh(KernelParams p, BvhArgs b,
@@ -1978,7 +2085,9 @@ hipError_t launch_bvh(const rtk::KernelParams* p, const rtk::BvhArgs* b, const r
     const bool lds_scene = (size_t)b->stack_depth * kBlockBvh * lds_entry + scene_bytes <= kLdsSceneBudget &&
                            (sizeof(StackEntry) == sizeof(int32_t) || refs16);
     const size_t stack_bytes = (size_t)b->stack_depth * kBlockBvh * (lds_scene ? sizeof(StackEntry) : sizeof(int32_t));
-    const size_t shmem = stack_bytes + (lds_scene ? scene_bytes : 0);
+    // + the waves' seed windows (kSeedWin, f64 kernel), 16-B aligned after the stacks
+    const size_t shmem = (((lds_scene ? scene_bytes : 0) + stack_bytes + 15) & ~(size_t)15) +
+                         (kF32 ? 0 : kSeedWinBlockBytes);
     const uint64_t need = (total + kBlockBvh - 1) / kBlockBvh;
     auto* st = (unsigned long long*)stats;
     auto launch = [&](auto kernel, const char* nm) -> hipError_t {

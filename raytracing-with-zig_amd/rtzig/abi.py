@@ -19,7 +19,7 @@ RT_OUT_LINEAR_F64 = 0
 RT_OUT_RGB8 = 1
 RT_PRECISION_F64 = 0
 RT_PRECISION_F32 = 1
-RT_PROFILE_STATS_WORDS = 64  # uint64 words of an instrumented render's d_stats (rt.h)
+RT_PROFILE_STATS_WORDS = 72  # uint64 words of an instrumented render's d_stats (rt.h)
 
 D3 = C.c_double * 3
 
