@@ -189,7 +189,7 @@ typedef int32_t StackEntry;
 #endif
 constexpr bool kSeedWin = RTZIG_SEED_WIN != 0;
 constexpr uint32_t kSeedWinPlanes = 14;
-constexpr uint32_t kSeedWinBytes = kSeedWinPlanes * 64 * 4;
+constexpr uint32_t kSeedWinBytes = kSeedWinPlanes * 64 * 4 + 16;  // + the window's key (16-B aligned)
 // LDS of one block: its share of a CU's 160 KiB at 16 waves per CU (2 blocks of 512 threads, or one
 // of 1024), less its waves' seed windows; the rest holds the tree + stacks when they fit
 constexpr size_t kLdsBlockShare = (size_t)160 * 1024 * (size_t)kBlockBvh / 1024;

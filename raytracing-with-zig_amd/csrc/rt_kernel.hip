@@ -98,18 +98,18 @@ __device__ __forceinline__ bool camera_start(uint32_t i, uint32_t j, Rng& g, Ray
 // The seed window's half of camera_start: sampleSquare's draws and the pixel sample point
 // (camera.zig:190-193, 203-209), the same operations as above.
 __device__ __forceinline__ v3 pixel_sample_point(uint32_t i, uint32_t j, Rng& g) {
-    u32x16 A;  // dwords 6..21 of KernelParams: center, pixel0, du.x, du.y
-    u32x8 B;   // dwords 22..29: du.z, dv
+    u32x16 A;  // dwords 12..27 of KernelParams: pixel0, du, dv.x, dv.y
+    u32x2 B;   // dwords 28..29: dv.z
     const uint64_t kp = (uint64_t)__builtin_amdgcn_kernarg_segment_ptr();
     asm volatile(
-        "s_load_dwordx16 %0, %2, 24\n\t"
-        "s_load_dwordx8 %1, %2, 88\n\t"
+        "s_load_dwordx16 %0, %2, 48\n\t"
+        "s_load_dwordx2 %1, %2, 112\n\t"
         "s_waitcnt lgkmcnt(0)"
         : "=s"(A), "=s"(B)
         : "s"(kp));
-    const v3 p0 = mk(dw2d(A[6], A[7]), dw2d(A[8], A[9]), dw2d(A[10], A[11]));
-    const v3 du = mk(dw2d(A[12], A[13]), dw2d(A[14], A[15]), dw2d(B[0], B[1]));
-    const v3 dv = mk(dw2d(B[2], B[3]), dw2d(B[4], B[5]), dw2d(B[6], B[7]));
+    const v3 p0 = mk(dw2d(A[0], A[1]), dw2d(A[2], A[3]), dw2d(A[4], A[5]));
+    const v3 du = mk(dw2d(A[6], A[7]), dw2d(A[8], A[9]), dw2d(A[10], A[11]));
+    const v3 dv = mk(dw2d(A[12], A[13]), dw2d(A[14], A[15]), dw2d(B[0], B[1]));
     const double ox = g.uniform() - 0.5;
     const double oy = g.uniform() - 0.5;
     return (p0 + muls(du, (double)i + ox)) + muls(dv, (double)j + oy);
@@ -1365,8 +1365,16 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
     uint32_t sh_kind = 3;  // kProf: this iteration's shading branch (0 sky, 1 Lambertian / metal, 2 dielectric, 3 none)
     uint32_t n_fill = 0, n_take = 0;  // kLanes: seed-window fills / take passes (stats[64], [65])
     uint64_t rt_start = 0, rt_drain = 0;  // s_memrealtime (100 MHz) at start / first empty claim (kProf only)
-    // the seed window's key (wave-uniform): the 64 pixels 64 * win_t + l of the launch at sample win_s
-    uint32_t win_t = ~0u, win_s = ~0u;
+    // the seed window's key, {t, s}: the 64 pixels 64 * t + l of the launch at sample s, kept in LDS
+    // after the window's planes (held in SGPRs, the pair pushed other uniform values into spills)
+    typedef __attribute__((address_space(3))) uint32_t lds_u32;
+    lds_u32* const wkey = (lds_u32*)(uintptr_t)(win + kSeedWinPlanes * 256);
+    if constexpr (kWin && !kF32) {
+        if (lane == 0) {
+            wkey[0] = ~0u;
+            wkey[1] = ~0u;
+        }
+    }
     if constexpr (kProf) rt_start = __builtin_amdgcn_s_memrealtime();
 
     // Head fold: the previous deferred call's reduce pass (rt_render_rows_async_deferred) is started
@@ -1425,18 +1433,20 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
             // holds another: a hand-out that crosses a sample layer or a unit takes two passes.
             // Every lane's generator is seeded and drawn exactly as camera_start does, so the bits
             // are unchanged.
-            typedef __attribute__((address_space(3))) uint32_t lds_u32;
             lds_u32* wp = (lds_u32*)(uintptr_t)win;
             uint64_t todo = __ballot(fresh);
             while (todo != 0) {
                 const uint32_t ld = (uint32_t)__builtin_ctzll(todo);
                 const uint32_t kt = __builtin_amdgcn_readlane(fq >> 6, ld);
                 const uint32_t ks = __builtin_amdgcn_readlane(fs, ld);
-                if (kt != win_t || ks != win_s) {
+                const uint32_t ht = __builtin_amdgcn_readfirstlane(wkey[0]), hs = __builtin_amdgcn_readfirstlane(wkey[1]);
+                if (kt != ht || ks != hs) {
                     RTK_MARK("win_fill");
                     if constexpr (kLanes) ++n_fill;
-                    win_t = kt;
-                    win_s = ks;
+                    if (lane == 0) {
+                        wkey[0] = kt;
+                        wkey[1] = ks;
+                    }
                     const uint32_t q = kt * 64 + lane;  // past the launch's last pixel: computed, never read
                     const uint32_t row_local = fastdiv(q, p.div_width);
                     const uint32_t i = q - row_local * W;
