@@ -114,9 +114,10 @@ __device__ __forceinline__ v3 pixel_sample_point(uint32_t i, uint32_t j, Rng& g)
     const double oy = g.uniform() - 0.5;
     return (p0 + muls(du, (double)i + ox)) + muls(dv, (double)j + oy);
 }
-// ... and the rest, for a fresh lane given its window entry: the ray from the camera center
-// (defocus: the direction holds the sample point until camera_finish adds the disk sample)
-__device__ __forceinline__ bool camera_from_point(const v3& ps, Ray& r) {
+// ... and the rest of camera_start: the ray's direction from the camera center (with defocus, the
+// sample point itself, until camera_finish adds the disk sample) and whether the disk sample is
+// pending; the window stores the direction, a fresh lane takes the origin
+__device__ __forceinline__ v3 camera_center(bool& defocus) {
     u32x8 A;  // dwords 6..13: center (+2 unused)
     u32x2 C;  // dwords 42..43: defocus_angle
     const uint64_t kp = (uint64_t)__builtin_amdgcn_kernarg_segment_ptr();
@@ -126,14 +127,8 @@ __device__ __forceinline__ bool camera_from_point(const v3& ps, Ray& r) {
         "s_waitcnt lgkmcnt(0)"
         : "=s"(A), "=s"(C)
         : "s"(kp));
-    const v3 center = mk(dw2d(A[0], A[1]), dw2d(A[2], A[3]), dw2d(A[4], A[5]));
-    r.orig = center;
-    if (dw2d(C[0], C[1]) <= 0) {
-        r.dir = ps - center;
-        return false;
-    }
-    r.dir = ps;
-    return true;
+    defocus = !(dw2d(C[0], C[1]) <= 0);
+    return mk(dw2d(A[0], A[1]), dw2d(A[2], A[3]), dw2d(A[4], A[5]));
 }
 // rayOrigin = defocusDiskSample() = (center + defocusDiskU * p.x) + defocusDiskV * p.y;
 // rayDirection = pixelSample - rayOrigin
@@ -1454,8 +1449,11 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
                     Rng gw;
                     gw.seed(sample_key(p.seed_mix, (uint64_t)j * W + i, ks));
                     const v3 ps = pixel_sample_point(i, j, gw);
-                    const uint64_t w[7] = {gw.s0, gw.s1, gw.s2, gw.s3, __builtin_bit_cast(uint64_t, ps.x),
-                                           __builtin_bit_cast(uint64_t, ps.y), __builtin_bit_cast(uint64_t, ps.z)};
+                    bool defocus;
+                    const v3 center = camera_center(defocus);
+                    const v3 dir = defocus ? ps : ps - center;  // camera_start's ray.dir
+                    const uint64_t w[7] = {gw.s0, gw.s1, gw.s2, gw.s3, __builtin_bit_cast(uint64_t, dir.x),
+                                           __builtin_bit_cast(uint64_t, dir.y), __builtin_bit_cast(uint64_t, dir.z)};
 #pragma unroll
                     for (int k = 0; k < 7; ++k) {
                         wp[(2 * k) * 64 + lane] = (uint32_t)w[k];
@@ -1475,9 +1473,11 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
                     g.s1 = w[1];
                     g.s2 = w[2];
                     g.s3 = w[3];
-                    dpend = camera_from_point(mk(__builtin_bit_cast(double, w[4]), __builtin_bit_cast(double, w[5]),
-                                                 __builtin_bit_cast(double, w[6])),
-                                              r);
+                    bool defocus;
+                    r.orig = camera_center(defocus);
+                    r.dir = mk(__builtin_bit_cast(double, w[4]), __builtin_bit_cast(double, w[5]),
+                               __builtin_bit_cast(double, w[6]));
+                    dpend = defocus;
                     att = V{1, 1, 1};
                     bounce = 0;
                 }

@@ -22,6 +22,8 @@
 #   dropin     the drop-in's one-shot cost per fresh process (tools/dropin_cold.py)  [DROPIN_CONFIGS]
 #   peak       event-timed VALU peak and issue-cost table (tools/bin/peak_rates, built beforehand)
 #   diag       bounds-checked builds through tools/diag_modes.py (ab/bounds*.so)
+#   uselib     copy $LIB (an ab/*.so build) over the in-tree librtzig.so for the steps after it (on the
+#              box's copy of the tree only)                                     [LIB]
 cd "$GRAFT_REPO_ROOT" 2>/dev/null || cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -53,6 +55,7 @@ for step in "$@"; do
     dropin)  run dropin 300 python3 -u tools/dropin_cold.py --runs 3 --configs ${DROPIN_CONFIGS:-2,4,5} ;;
     peak)    run peak 300 ./tools/bin/peak_rates ${PEAK_MS:-60} ${PEAK_MODE:-2} ;;
     diag)    run diag 300 python3 -u tools/diag_modes.py raytracing-with-zig_amd/librtzig.so ab/bounds.so --oracle-row ;;
+    uselib)  cp "$LIB" raytracing-with-zig_amd/librtzig.so || exit 2; echo "== using $LIB" ;;
     *) echo "unknown step: $step"; exit 2 ;;
   esac
 done
