@@ -167,12 +167,12 @@ struct KernelParams {
 // spread over the whole bank row.  Leaves (2 slots: 80 B = 5 x 16, read as ds_read_b128) start
 // at the next 16-B boundary after the nodes.
 #ifndef RTZIG_BVH_BLOCK
-#define RTZIG_BVH_BLOCK 512
+#define RTZIG_BVH_BLOCK 1024
 #endif
 #ifndef RTZIG_STACK16
 #define RTZIG_STACK16 0
 #endif
-constexpr int kBlockBvh = RTZIG_BVH_BLOCK;  // 8 waves; 2 blocks per CU share the LDS budget (build knob)
+constexpr int kBlockBvh = RTZIG_BVH_BLOCK;  // threads of the BVH kernels' blocks (build knob)
 // per-lane stack entry of the BVH walk (build knob: int16 holds every ref of a tree whose nodes and
 // leaves each span < 32 KiB, rt_kernel.hip StackOps)
 #if RTZIG_STACK16
@@ -185,7 +185,7 @@ typedef int32_t StackEntry;
 // fresh lane seeding its own (≈21 of 64 lanes active).  Per wave: 14 dword planes of 64 lanes
 // (Xoshiro s0..s3 after sampleSquare's two draws, the pixel sample point): 3.5 KiB.
 #ifndef RTZIG_SEED_WIN
-#define RTZIG_SEED_WIN 0
+#define RTZIG_SEED_WIN 1
 #endif
 constexpr bool kSeedWin = RTZIG_SEED_WIN != 0;
 constexpr uint32_t kSeedWinPlanes = 14;
@@ -195,6 +195,14 @@ constexpr uint32_t kSeedWinBytes = kSeedWinPlanes * 64 * 4 + 16;  // + the windo
 constexpr size_t kLdsBlockShare = (size_t)160 * 1024 * (size_t)kBlockBvh / 1024;
 constexpr size_t kSeedWinBlockBytes = kSeedWin ? (size_t)(kBlockBvh / 64) * kSeedWinBytes : 0;
 constexpr size_t kLdsSceneBudget = kLdsBlockShare - kSeedWinBlockBytes;  // tree + stacks of one block
+// The instrumented BVH kernels (kProf) run 512-thread blocks whatever kBlockBvh is: their counters
+// need more than the 128 VGPRs a 1024-thread block allows (4 waves per SIMD) and would spill to
+// scratch; at 512 threads they keep 3 waves per SIMD.  Their LDS budget is a whole CU's, less their
+// seed windows (one block per CU when the tree is in LDS).
+constexpr int kBlockBvhProf = 512;
+constexpr size_t kSeedWinProfBytes = kSeedWin ? (size_t)(kBlockBvhProf / 64) * kSeedWinBytes : 0;
+constexpr size_t kLdsSceneBudgetProf = (size_t)160 * 1024 - kSeedWinProfBytes;
+__host__ __device__ constexpr int bvh_block(bool prof) { return prof ? kBlockBvhProf : kBlockBvh; }
 constexpr int kMaxDepthBvh = 16;   // == rtbvh::kMaxDepth: bound on per-lane LDS stack entries (entry 0: "done")
 #ifndef RTZIG_LEAF
 #define RTZIG_LEAF 2

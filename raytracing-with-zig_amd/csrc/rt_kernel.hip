@@ -489,7 +489,7 @@ constexpr int32_t kDone = INT32_MIN;  // walk finished (stack entry 0)
 // keep their walk state (BvhWalker::State, the stack stays in LDS) and resume in the next
 // iteration, while the free lanes shade and start their next segment.
 #ifndef RTZIG_REFETCH_K
-#define RTZIG_REFETCH_K 56
+#define RTZIG_REFETCH_K 52
 #endif
 constexpr int kRefetchK = RTZIG_REFETCH_K;
 // Drain mode (RTZIG_DRAIN, default 0: an A/B knob, measured within noise and not adopted): once a
@@ -1893,13 +1893,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kWaves))
 #endif
 #define RTK_BVH_BODY(kF32) \
     /* LDS: [nodes][leaves] (kLdsScene) at address 0, so a node's byte-offset ref IS its LDS */ \
-    /* address; then the per-lane stacks [kMaxDepthBvh][kBlockBvh] */ \
+    /* address; then the per-lane stacks [stack_depth][kB]; then the waves' seed windows */ \
+    constexpr int kB = bvh_block(kProf); \
     extern __shared__ __align__(16) unsigned char lds_raw[]; \
     const size_t scene_bytes = \
         kLdsScene ? (size_t)bvh_leaves_offset(b.n_nodes) + (size_t)b.n_leaves * sizeof(BvhLeaf) : 0; \
     /* the int16 stack (RTZIG_STACK16) needs every ref in LDS range: the global-memory tree uses int32 */ \
     using Stack = std::conditional_t<kLdsScene, StackEntry, int32_t>; \
-    using Walker = BvhWalker<kLdsScene, kBlockBvh, Stack, kF32>; \
+    using Walker = BvhWalker<kLdsScene, kB, Stack, kF32>; \
     Stack* stack = (Stack*)(lds_raw + scene_bytes); \
     stack[threadIdx.x] = (Stack)Walker::kEnd;  /* entry 0 of this lane's stack: popping it ends the walk */ \
     const BvhNode* nodes = b.nodes; \
@@ -1913,16 +1914,17 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kWaves))
         nodes = ln; \
         leaves = ll; \
     } \
-    /* the wave's seed window after the stacks (kSeedWin, f64 kernels) */ \
+    /* the wave's seed window after the stacks (kSeedWin: the f64 kernels with the tree in LDS; the */ \
+    /* global-memory tree kernels for large scenes keep per-lane seeding, which fits 128 VGPRs) */ \
     const uint32_t win = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) unsigned char*)( \
-        lds_raw + ((scene_bytes + (size_t)b.stack_depth * kBlockBvh * sizeof(Stack) + 15) & ~(size_t)15) + \
+        lds_raw + ((scene_bytes + (size_t)b.stack_depth * kB * sizeof(Stack) + 15) & ~(size_t)15) + \
         (threadIdx.x / 64) * kSeedWinBytes); \
-    path_loop<kProf, kDirect, kSeedWin && !kF32>(p, Walker{nodes, leaves, b.always_geo, b.always_sid, b.n_always, \
+    path_loop<kProf, kDirect, kSeedWin && !kF32 && kLdsScene>(p, Walker{nodes, leaves, b.always_geo, b.always_sid, b.n_always, \
                                          stack + threadIdx.x, b.origin_bound, geo_g, p.n_pad RTK_BOUNDS_ARGS}, geo_g, \
                               mat_g, ua, stats, win);
 
 template <bool kLdsScene, bool kProf, bool kDirect>
-__global__ __launch_bounds__(kBlockBvh) RTK_BVH_WAVES void sample_kernel_bvh(KernelParams p, BvhArgs b,
+__global__ __launch_bounds__(bvh_block(kProf)) RTK_BVH_WAVES void sample_kernel_bvh(KernelParams p, BvhArgs b,
                                                                const GeoRec* __restrict__ geo_g,
                                                                const MatRec* __restrict__ mat_g, UnitArgs ua,
                                                                unsigned long long* __restrict__ stats) {
@@ -1932,7 +1934,7 @@ __global__ __launch_bounds__(kBlockBvh) RTK_BVH_WAVES void sample_kernel_bvh(Ker
 // (4 waves per SIMD; left alone its ring-mode instantiation takes 131 VGPRs, i.e. 3 waves; the
 // instrumented builds 3, as for the parity kernel; RTZIG_BVH_WAVES overrides both)
 template <bool kLdsScene, bool kProf, bool kDirect>
-__global__ __launch_bounds__(kBlockBvh) RTK_BVH_WAVES void sample_kernel_fast(
+__global__ __launch_bounds__(bvh_block(kProf)) RTK_BVH_WAVES void sample_kernel_fast(
     KernelParams p, BvhArgs b, const GeoRec* __restrict__ geo_g, const MatRec* __restrict__ mat_g, UnitArgs ua,
     unsigned long long* __restrict__ stats) {
     RTK_BVH_BODY(true)
@@ -2087,33 +2089,35 @@ hipError_t launch_bvh(const rtk::KernelParams* p, const rtk::BvhArgs* b, const r
     const uint64_t total = (uint64_t)p->n_rows * p->width * p->s_count;
     if (total == 0) return hipSuccess;
     if (b->stack_depth < 2 || b->stack_depth > (uint32_t)kMaxDepthBvh) return hipErrorInvalidValue;
+    const bool prof = p->prof != 0;
+    const uint32_t block = (uint32_t)bvh_block(prof);
     const size_t scene_bytes = (size_t)bvh_leaves_offset(b->n_nodes) + (size_t)b->n_leaves * sizeof(BvhLeaf);
     // int16 stack entries (RTZIG_STACK16) hold node and leaf byte offsets below 2^15
     const bool refs16 = bvh_leaves_offset(b->n_nodes) < 32768u && (size_t)b->n_leaves * sizeof(BvhLeaf) < 32768u;
     const size_t lds_entry = refs16 ? sizeof(StackEntry) : sizeof(int32_t);
-    // scene in LDS when two blocks still fit a CU's 160 KiB
-    const bool lds_scene = (size_t)b->stack_depth * kBlockBvh * lds_entry + scene_bytes <= kLdsSceneBudget &&
+    // scene in LDS when the block's share of a CU holds tree + stacks + seed windows (kLdsSceneBudget)
+    const bool lds_scene = (size_t)b->stack_depth * block * lds_entry + scene_bytes <=
+                               (prof ? kLdsSceneBudgetProf : kLdsSceneBudget) &&
                            (sizeof(StackEntry) == sizeof(int32_t) || refs16);
-    const size_t stack_bytes = (size_t)b->stack_depth * kBlockBvh * (lds_scene ? sizeof(StackEntry) : sizeof(int32_t));
-    // + the waves' seed windows (kSeedWin, f64 kernel), 16-B aligned after the stacks
+    const size_t stack_bytes = (size_t)b->stack_depth * block * (lds_scene ? sizeof(StackEntry) : sizeof(int32_t));
+    // + the waves' seed windows (kSeedWin, the f64 kernel with the tree in LDS), 16-B aligned after the stacks
     const size_t shmem = (((lds_scene ? scene_bytes : 0) + stack_bytes + 15) & ~(size_t)15) +
-                         (kF32 ? 0 : kSeedWinBlockBytes);
-    const uint64_t need = (total + kBlockBvh - 1) / kBlockBvh;
+                         (kF32 || !lds_scene ? 0 : (prof ? kSeedWinProfBytes : kSeedWinBlockBytes));
+    const uint64_t need = (total + block - 1) / block;
     auto* st = (unsigned long long*)stats;
     auto launch = [&](auto kernel, const char* nm) -> hipError_t {
         uint32_t cap32 = 0;
-        const hipError_t ea = rtk_resident_blocks((const void*)kernel, kBlockBvh, shmem, &cap32);
+        const hipError_t ea = rtk_resident_blocks((const void*)kernel, (int)block, shmem, &cap32);
         if (ea != hipSuccess) return ea;
         if (plan_waves) {
-            *plan_waves = plan_of(need, cap32, kBlockBvh);
+            *plan_waves = plan_of(need, cap32, block);
             return hipSuccess;
         }
-        const uint32_t blocks = grid_blocks(need, cap32, ua, kBlockBvh);
+        const uint32_t blocks = grid_blocks(need, cap32, ua, block);
         if (name) *name = nm;
-        hipLaunchKernelGGL(kernel, dim3(blocks), dim3(kBlockBvh), shmem, stream, *p, *b, geo, mat, *ua, st);
+        hipLaunchKernelGGL(kernel, dim3(blocks), dim3(block), shmem, stream, *p, *b, geo, mat, *ua, st);
         return hipGetLastError();
     };
-    const bool prof = p->prof != 0;
 #define RTK_BVH(L, PR, D, NM)                                                                          \
     if (lds_scene == L && prof == PR && direct == D) {                                                 \
         if constexpr (kF32) return launch(sample_kernel_fast<L, PR, D>, NM);                           \

@@ -46,6 +46,8 @@ def lanes_of(s):
         "shade_dielectric": row(s[46], s[47]),
         "store": row(s[48], s[49]),
         "lanes_holding_a_path_per_iteration": row(s[26], s[50]),
+        **({"seed_window": {"fills": s[64], "take_passes": s[65], "fresh_lanes_per_take": round(s[32] / s[65], 3),
+                            "samples_per_fill": round(s[1] / s[64], 3)}} if len(s) > 65 and s[64] else {}),
     }
 
 

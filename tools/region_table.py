@@ -208,12 +208,15 @@ def main():
         acw, acl = [g(54 + q) for q in range(4)], [g(58 + q) for q in range(4)]
         lcw, lcl = g(9) - sum(acw), g(52) - sum(acl)
         ratio = lambda l, w: l / w if w else 0.0  # noqa: E731
+        if len(raw) > 65 and raw[64]:  # seed-window builds: fills at 64 lanes, take passes at the fresh lanes
+            W.update({"win_fill": g(64), "seed": g(65)})
+            LN.update({"win_fill": full})
         W.update({"walk_setup": g(38), "always": n["wstart"], "cam_finish": g(36), "scat_finish": g(34),
                   "sky": g(42), "lam_metal": g(44), "dielectric": g(46), "store": g(48), "aroot2N": 0.0, "acandN": 0.0})
         for q in range(4):
             W[f"acand{q}"] = acw[q]
             LN[f"acand{q}"] = ratio(acl[q], acw[q])
-        LN.update({"seed": ratio(g(32), g(28)), "trips": ratio(g(33), g(27)), "cam_finish": ratio(g(37), g(36)),
+        LN.update({"seed": ratio(g(32), g(65) if len(raw) > 65 and raw[64] else g(28)), "trips": ratio(g(33), g(27)), "cam_finish": ratio(g(37), g(36)),
                    "scat_finish": ratio(g(35), g(34)), "walk_setup": ratio(g(39), g(38)), "always": ratio(g(40), g(29)),
                    "walk_inner": ratio(g(3), g(7)), "walk_inner_other": ratio(g(39), g(38)), "leaf": ratio(g(51), g(8)),
                    "lcand": ratio(lcl, lcw), "aroot2": ratio(g(63), g(62)), "lroot2": ratio(g(53) - g(63), g(10) - g(62)),
@@ -308,7 +311,7 @@ def main():
             if not re.match(r"^v_(add|mul|fma|fmac)_f64|^v_(rsq|rcp|sqrt|exp|log|sin|cos)_f(32|64)", op):
                 other["n"] += w
                 other["cyc"] += w * rt
-    order = ["finalise", "fin_work", "handout", "seed", "idle", "trips", "scatter_finish", "cam_finish", "scat_finish",
+    order = ["finalise", "fin_work", "handout", "seed", "win_fill", "idle", "trips", "scatter_finish", "cam_finish", "scat_finish",
              "walk_setup", "always", "acand0", "acand1", "acand2", "acand3", "acandN", "aroot2", "aroot2N", "walk_inner",
              "leaf", "lcand", "lroot2", "shade", "sky", "lam_metal", "dielectric", "store", "rare", "prologue", "epilogue", "?"]
     rows = []
