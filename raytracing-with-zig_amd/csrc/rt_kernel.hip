@@ -1868,7 +1868,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kWaves))
         __syncthreads();
         geo = lds_geo;
     }
-    path_loop<kProf, kDirect>(p, LinearWalker<U>{geo, p.n_pad, p.n_spheres}, geo, mat_g, ua, stats);
+    // the waves' seed windows after the LDS geometry (kSeedWin; rtk_launch_samples sizes the LDS)
+    const uint32_t win = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) unsigned char*)(
+        (unsigned char*)lds_geo + (kLds ? (size_t)p.n_pad * sizeof(GeoRec) : 0) + (threadIdx.x / 64) * kSeedWinBytes);
+    path_loop<kProf, kDirect, kSeedWin>(p, LinearWalker<U>{geo, p.n_pad, p.n_spheres}, geo, mat_g, ua, stats, win);
 }
 
 // BVH-walk kernel: nodes + slot geometry + slot ids staged in LDS (kLdsScene) or read from global
@@ -2066,7 +2069,7 @@ extern "C" hipError_t rtk_launch_samples(const rtk::KernelParams* p, const rtk::
     const uint64_t total = (uint64_t)p->n_rows * p->width * p->s_count;
     if (total == 0) return hipSuccess;
     const Variant& v = variant_choice(p->n_pad <= kMaxLdsSpheres, p->n_pad);
-    const size_t shmem = v.lds ? (size_t)p->n_pad * sizeof(GeoRec) : 0;
+    const size_t shmem = (v.lds ? (size_t)p->n_pad * sizeof(GeoRec) : 0) + (kSeedWin ? (kBlock / 64) * kSeedWinBytes : 0);
     const uint64_t need = (total + kBlock - 1) / kBlock;
     auto* st = (unsigned long long*)stats;
     if (name) *name = v.name;
