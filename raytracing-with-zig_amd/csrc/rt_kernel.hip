@@ -16,7 +16,8 @@
 //   accumulates each pixel's samples in sample order inside the kernel (wave rings + running sums
 //   handed from wave to wave); direct mode (small launches) stores every sample for the reduce pass.
 //   The closest hit is HittableList.hit's first-wins argmin, found by a BVH walk over an LDS-resident
-//   tree (BvhWalker) or the reference's list walk (LinearWalker) with the same f64 quadratic.
+//   tree (BvhWalker) or the reference's list walk (LinearWalker) with the same f64 quadratic.  New
+//   items are seeded 64 at a time by the whole wave into an LDS seed window (kSeedWin, path_loop).
 //
 // reduce_kernel — direct mode only: per pixel, adds the stored sample colours in sample order
 //   (camera.zig:135 `pixelColor += rayColor(ray)`, the same sequence of roundings as the reference's
