@@ -232,6 +232,20 @@ __device__ __forceinline__ bool camera_start(uint32_t i, uint32_t j, Rng& g, fm:
     r.dir = ps;
     return true;
 }
+// fast mode's camera center and defocus flag (fcam), for a fresh lane given its seed-window entry
+__device__ __forceinline__ fm::f3 camera_center_f32(bool& defocus) {
+    u32x4 B;  // fcam[16..19]
+    u32x4 A;  // fcam[0..3]
+    const uint64_t kp = (uint64_t)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile(
+        "s_load_dwordx4 %0, %2, %3\n\t"
+        "s_load_dwordx4 %1, %2, %4\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=s"(A), "=s"(B)
+        : "s"(kp), "i"(kFcam), "i"(kFcam + 64));
+    defocus = !(fw(B[2]) <= 0);
+    return fm::mk(fw(A[0]), fw(A[1]), fw(A[2]));
+}
 __device__ __forceinline__ void camera_finish(float px, float py, fm::Ray& r) {
 #pragma clang fp contract(fast)
     u32x16 A;
@@ -1365,7 +1379,7 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
     // after the window's planes (held in SGPRs, the pair pushed other uniform values into spills)
     typedef __attribute__((address_space(3))) uint32_t lds_u32;
     lds_u32* const wkey = (lds_u32*)(uintptr_t)(win + kSeedWinPlanes * 256);
-    if constexpr (kWin && !kF32) {
+    if constexpr (kWin) {
         if (lane == 0) {
             wkey[0] = ~0u;
             wkey[1] = ~0u;
@@ -1421,7 +1435,7 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
             l_busy += (uint32_t)__popcll(__ballot(active));
         }
         RTK_MARK("seed");
-        if constexpr (kWin && !kF32) {
+        if constexpr (kWin) {
             // Seed window: the fresh lanes' items are (pixel fq, sample fs); the window holds the
             // generators (after sampleSquare's draws) and pixel sample points of the 64 pixels
             // 64 * win_t + l at sample win_s, computed by all 64 lanes at once.  Each pass serves
@@ -1449,12 +1463,27 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
                     const uint32_t j = p.row0 + row_local * p.row_step;
                     Rng gw;
                     gw.seed(sample_key(p.seed_mix, (uint64_t)j * W + i, ks));
-                    const v3 ps = pixel_sample_point(i, j, gw);
-                    bool defocus;
-                    const v3 center = camera_center(defocus);
-                    const v3 dir = defocus ? ps : ps - center;  // camera_start's ray.dir
-                    const uint64_t w[7] = {gw.s0, gw.s1, gw.s2, gw.s3, __builtin_bit_cast(uint64_t, dir.x),
-                                           __builtin_bit_cast(uint64_t, dir.y), __builtin_bit_cast(uint64_t, dir.z)};
+                    uint64_t w[7];
+                    if constexpr (kF32) {  // fast mode: camera_start's f32 ray direction (2 planes unused)
+                        fm::Ray rw;
+                        (void)camera_start(i, j, gw, rw);
+                        w[4] = (uint64_t)__builtin_bit_cast(uint32_t, rw.dir.x) |
+                               ((uint64_t)__builtin_bit_cast(uint32_t, rw.dir.y) << 32);
+                        w[5] = __builtin_bit_cast(uint32_t, rw.dir.z);
+                        w[6] = 0;
+                    } else {
+                        const v3 ps = pixel_sample_point(i, j, gw);
+                        bool defocus;
+                        const v3 center = camera_center(defocus);
+                        const v3 dir = defocus ? ps : ps - center;  // camera_start's ray.dir
+                        w[4] = __builtin_bit_cast(uint64_t, dir.x);
+                        w[5] = __builtin_bit_cast(uint64_t, dir.y);
+                        w[6] = __builtin_bit_cast(uint64_t, dir.z);
+                    }
+                    w[0] = gw.s0;
+                    w[1] = gw.s1;
+                    w[2] = gw.s2;
+                    w[3] = gw.s3;
 #pragma unroll
                     for (int k = 0; k < 7; ++k) {
                         wp[(2 * k) * 64 + lane] = (uint32_t)w[k];
@@ -1475,9 +1504,15 @@ __device__ __forceinline__ void path_loop(const KernelParams& p, const Walker& w
                     g.s2 = w[2];
                     g.s3 = w[3];
                     bool defocus;
-                    r.orig = camera_center(defocus);
-                    r.dir = mk(__builtin_bit_cast(double, w[4]), __builtin_bit_cast(double, w[5]),
-                               __builtin_bit_cast(double, w[6]));
+                    if constexpr (kF32) {
+                        r.orig = camera_center_f32(defocus);
+                        r.dir = fm::mk(__builtin_bit_cast(float, (uint32_t)w[4]), __builtin_bit_cast(float, (uint32_t)(w[4] >> 32)),
+                                       __builtin_bit_cast(float, (uint32_t)w[5]));
+                    } else {
+                        r.orig = camera_center(defocus);
+                        r.dir = mk(__builtin_bit_cast(double, w[4]), __builtin_bit_cast(double, w[5]),
+                                   __builtin_bit_cast(double, w[6]));
+                    }
                     dpend = defocus;
                     att = V{1, 1, 1};
                     bounce = 0;
@@ -1918,12 +1953,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kWaves))
         nodes = ln; \
         leaves = ll; \
     } \
-    /* the wave's seed window after the stacks (kSeedWin: the f64 kernels with the tree in LDS; the */ \
+    /* the wave's seed window after the stacks (kSeedWin: the kernels with the tree in LDS; the */ \
     /* global-memory tree kernels for large scenes keep per-lane seeding, which fits 128 VGPRs) */ \
     const uint32_t win = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) unsigned char*)( \
         lds_raw + ((scene_bytes + (size_t)b.stack_depth * kB * sizeof(Stack) + 15) & ~(size_t)15) + \
         (threadIdx.x / 64) * kSeedWinBytes); \
-    path_loop<kProf, kDirect, kSeedWin && !kF32 && kLdsScene>(p, Walker{nodes, leaves, b.always_geo, b.always_sid, b.n_always, \
+    path_loop<kProf, kDirect, kSeedWin && kLdsScene>(p, Walker{nodes, leaves, b.always_geo, b.always_sid, b.n_always, \
                                          stack + threadIdx.x, b.origin_bound, geo_g, p.n_pad RTK_BOUNDS_ARGS}, geo_g, \
                               mat_g, ua, stats, win);
 
@@ -2106,7 +2141,7 @@ hipError_t launch_bvh(const rtk::KernelParams* p, const rtk::BvhArgs* b, const r
     const size_t stack_bytes = (size_t)b->stack_depth * block * (lds_scene ? sizeof(StackEntry) : sizeof(int32_t));
     // + the waves' seed windows (kSeedWin, the f64 kernel with the tree in LDS), 16-B aligned after the stacks
     const size_t shmem = (((lds_scene ? scene_bytes : 0) + stack_bytes + 15) & ~(size_t)15) +
-                         (kF32 || !lds_scene ? 0 : (prof ? kSeedWinProfBytes : kSeedWinBlockBytes));
+                         (!lds_scene ? 0 : (prof ? kSeedWinProfBytes : kSeedWinBlockBytes));
     const uint64_t need = (total + block - 1) / block;
     auto* st = (unsigned long long*)stats;
     auto launch = [&](auto kernel, const char* nm) -> hipError_t {

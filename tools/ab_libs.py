@@ -32,6 +32,7 @@ ap.add_argument("--n-spheres", type=int, default=4000,
 ap.add_argument("--row-step", type=int, default=1,
                 help="render rank 0's interleaved row set of an N-rank job (rows 0, N, 2N, ...)")
 ap.add_argument("--no-check", action="store_true", help="ablation builds: skip the bit-equality check")
+ap.add_argument("--precision", choices=["f64", "f32"], default="f64", help="f32: fast mode (RT_PRECISION_F32)")
 args = ap.parse_args()
 
 if args.scene == "final":
@@ -72,6 +73,7 @@ for spec in args.libs:  # "lib.so" or "lib.so:VAR=VAL" (an environment variable 
                             ("rt_context_kernel_times", C.c_int, [vp, C.POINTER(C.c_double), C.POINTER(C.c_double)]),
                             ("rt_render_rows_async", C.c_int, [vp, C.POINTER(rtzig.RtCamera), C.c_uint32, C.c_uint32,
                                                                C.c_uint32, C.c_uint32, vp, vp, vp]),
+                            ("rt_context_set_precision", C.c_int, [vp, C.c_int]),
                             ("rt_last_error", C.c_char_p, [])]:
         getattr(L, name).restype = res
         getattr(L, name).argtypes = argt
@@ -83,6 +85,7 @@ for spec in args.libs:  # "lib.so" or "lib.so:VAR=VAL" (an environment variable 
     if envs[spec]:
         del os.environ[envs[spec][0]]
     assert L.rt_context_enable_timing(ctx, 1) == 0
+    assert L.rt_context_set_precision(ctx, 1 if args.precision == "f32" else 0) == 0, L.rt_last_error()
     runs.append((spec, L, ctx))
 times = {p: [] for p, _, _ in runs}
 rtimes = {p: [] for p, _, _ in runs}
